@@ -1,0 +1,34 @@
+// C ABI glue: error state and the GEMM entry point.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "fervit_internal.h"
+
+namespace fer {
+
+static thread_local char g_err[512] = "";
+
+int set_error(const char* msg) {
+  snprintf(g_err, sizeof(g_err), "%s", msg);
+  return -1;
+}
+
+int hip_check(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    snprintf(g_err, sizeof(g_err), "%s: %s", what, hipGetErrorString(e));
+    return -2;
+  }
+  return 0;
+}
+
+}  // namespace fer
+
+extern "C" const char* fer_last_error(void) { return fer::g_err; }
+extern "C" const char* fer_version(void) { return "fervit-mi355x 0.1 (gfx950)"; }
+
+extern "C" int fer_gemm(const fer_gemm_desc* d, const fer_epilogue* e, fer_stream_t stream) {
+  if (!d || !e) return fer::set_error("gemm: null descriptor");
+  return fer::gemm_launch(*d, *e, (hipStream_t)stream);
+}

@@ -1,0 +1,98 @@
+// Shared device-side helpers for the FER-ViT gfx950 kernels.
+//
+// Storage conventions:
+//   * activations are token-major [M = B*N rows][D cols], row-major, bf16 (fast path)
+//     or fp32 (parity path); weights follow nn.Linear's [out][in] layout.
+//   * bf16 is the compiler's __bf16 (lowered to v_cvt_pk_bf16_f32 on gfx950).
+//   * dropout keep-masks are never stored: they are regenerated from
+//     (seed, linear element index) by `drop_keep`, in forward and backward.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define FER_DEV __device__ __forceinline__
+
+typedef __bf16 bf16;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+typedef __attribute__((ext_vector_type(4))) short short4_t;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((address_space(3))) void lds_void;
+
+enum { FER_ACT_NONE = 0, FER_ACT_GELU = 1, FER_ACT_RELU = 2 };
+
+FER_DEV float bf2f(bf16 x) { return (float)x; }
+FER_DEV bf16 f2bf(float x) { return (bf16)x; }
+
+template <typename T> FER_DEV float to_f(T x);
+template <> FER_DEV float to_f<float>(float x) { return x; }
+template <> FER_DEV float to_f<bf16>(bf16 x) { return (float)x; }
+template <typename T> FER_DEV T from_f(float x);
+template <> FER_DEV float from_f<float>(float x) { return x; }
+template <> FER_DEV bf16 from_f<bf16>(float x) { return (bf16)x; }
+
+// 4 consecutive elements <-> float4 (8 B for bf16, 16 B for fp32).
+template <typename T> FER_DEV f32x4 load4(const T* p);
+template <> FER_DEV f32x4 load4<float>(const float* p) { return *(const f32x4*)p; }
+template <> FER_DEV f32x4 load4<bf16>(const bf16* p) {
+  bf16x4 v = *(const bf16x4*)p;
+  return f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
+}
+template <typename T> FER_DEV void store4(T* p, f32x4 v);
+template <> FER_DEV void store4<float>(float* p, f32x4 v) { *(f32x4*)p = v; }
+template <> FER_DEV void store4<bf16>(bf16* p, f32x4 v) {
+  *(bf16x4*)p = bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+}
+
+// ---------------------------------------------------------------- activations
+FER_DEV float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+FER_DEV float gelu_erf_grad(float x) {
+  const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
+  const float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
+  return cdf + x * pdf;
+}
+FER_DEV float act_fwd(int act, float x) {
+  return act == FER_ACT_GELU ? gelu_erf(x) : (act == FER_ACT_RELU ? fmaxf(x, 0.f) : x);
+}
+FER_DEV float act_grad(int act, float x) {
+  return act == FER_ACT_GELU ? gelu_erf_grad(x) : (act == FER_ACT_RELU ? (x > 0.f ? 1.f : 0.f) : 1.f);
+}
+
+// ---------------------------------------------------------------- dropout RNG
+// Counter-based: keep(seed, idx) is a pure function, so backward regenerates the
+// forward mask. 64-bit idx (tensors up to 2^64 elements), murmur3-style finaliser.
+FER_DEV uint32_t fer_hash(uint64_t seed, uint64_t idx) {
+  uint64_t z = idx + seed * 0x9E3779B97F4A7C15ull;
+  z ^= z >> 32;
+  z *= 0xD6E8FEB86659FD93ull;
+  z ^= z >> 32;
+  z *= 0xD6E8FEB86659FD93ull;
+  z ^= z >> 32;
+  return (uint32_t)z;
+}
+// thresh = p * 2^32 (0 => never drop)
+FER_DEV bool drop_keep(uint64_t seed, uint64_t idx, uint32_t thresh) {
+  return thresh == 0u || fer_hash(seed, idx) >= thresh;
+}
+
+// ---------------------------------------------------------------- reductions
+FER_DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+FER_DEV float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// ---------------------------------------------------------------- buffer rsrc
+// Raw buffer descriptor. Loads whose voffset >= num_records return 0: kernels
+// mask out-of-tile lanes by giving them FER_OOB as voffset.
+#define FER_OOB 0x80000000u
+FER_DEV __amdgpu_buffer_rsrc_t make_rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)0x7FFFFFF0, 0x00020000);
+}

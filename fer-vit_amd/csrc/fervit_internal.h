@@ -1,0 +1,30 @@
+// Internal host/device declarations shared by the kernel translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <algorithm>
+#include <stdint.h>
+
+#include "../../include/fervit.h"
+
+namespace fer {
+
+typedef fer_epilogue EpiArgs;
+typedef fer_gemm_desc GemmDesc;
+
+struct GemmArgs {
+  const void* A;
+  const void* B;
+  long lda, ldb;
+  int M, N, K;
+  int tiles_m, tiles_n;
+  int splits, k_chunk, partial;
+  float* ws;
+};
+
+int set_error(const char* msg);
+int hip_check(const char* what);
+int gemm_launch(const GemmDesc& d, const EpiArgs& e, hipStream_t st);
+
+inline int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
+
+}  // namespace fer

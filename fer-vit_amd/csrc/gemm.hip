@@ -1,0 +1,341 @@
+// GEMM family for every Linear / Conv-as-GEMM on the FER-ViT hot path.
+//
+//   C[m][n] = epilogue( sum_k A(m,k) * B(n,k) )
+//   A(m,k) = A[m*lda + k]  (A_KC, "K-contiguous")  or  A[k*lda + m]  (MN-contiguous)
+//   B(n,k) = B[n*ldb + k]  (B_KC)                  or  B[k*ldb + n]
+//
+// The three nn.Linear passes map onto it without any transposed copies:
+//   forward  Y  = X W^T      : A=X  (KC), B=W (KC)            (nn.Linear, `image_vit.py:101-113`)
+//   dgrad    dX = dY W       : A=dY (KC), B=W (MN)
+//   wgrad    dW = dY^T X     : A=dY (MN), B=X (MN), K = rows = B*N tokens (split-K)
+//
+// bf16 path: v_mfma_f32_16x16x32_bf16 (fp32 accumulate). A and B tiles are staged
+// global->LDS by LDS-DMA (buffer_load ... lds, 16 B/lane) with the swizzle applied on
+// the per-lane SOURCE address (the DMA image is lane-linear):
+//   KC image  [rows][64 k]  (128 B rows): chunk' = chunk ^ ((row>>1)&7)
+//   MN image  [64 k][rows]  (2*R B rows): chunk' = chunk ^ (rho(k)<<1),
+//                                          rho(k) = (k&3) | ((k>>3)&1)<<2
+// KC fragments are read with ds_read_b128, MN fragments with two ds_read_b64_tr_b16
+// (hardware transpose); both images are bank-conflict free for their reads.
+// Out-of-range rows/cols/k (tails) are zero-filled by the buffer range check.
+// The MFMA is issued with the B fragment as the instruction's A operand, so each
+// lane ends with 4 consecutive n of one m (8/16-byte epilogue accesses).
+//
+// fp32 path (parity mode): a plain LDS-tiled VALU kernel with the same epilogue.
+#include "common.h"
+#include "fervit_internal.h"
+
+namespace fer {
+
+// ------------------------------------------------------------------- epilogue
+template <typename T>
+FER_DEV void epi4(const EpiArgs& e, long m, long n, f32x4 v) {
+  v *= e.alpha;
+  if (e.bias) v += *(const f32x4*)(e.bias + n);
+  if (e.pre) store4<T>((T*)e.pre + m * e.ldp + n, v);
+  if (e.act) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = act_fwd(e.act, v[r]);
+  }
+  if (e.drop_thresh) {
+    const uint64_t base = (uint64_t)m * (uint64_t)e.drop_ld + (uint64_t)n;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = drop_keep(e.seed, base + r, e.drop_thresh) ? v[r] * e.drop_scale : 0.f;
+  }
+  if (e.aux) {
+    f32x4 a = load4<T>((const T*)e.aux + m * e.ldx + n);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] *= act_grad(e.aux_act, a[r]);
+  }
+  if (e.res) v += load4<T>((const T*)e.res + m * e.ldr + n);
+  if (e.c_f32) {
+    float* c = (float*)e.c + m * e.ldc + n;
+    if (e.accumulate) v += *(const f32x4*)c;
+    *(f32x4*)c = v;
+  } else {
+    T* c = (T*)e.c + m * e.ldc + n;
+    if (e.accumulate) v += load4<T>(c);
+    store4<T>(c, v);
+  }
+}
+
+// ------------------------------------------------------------ tile scheduling
+// XCD-aware, bijective remap (blocks b and b+8 share an XCD under round-robin
+// dispatch) followed by GROUP_M-row grouping for L2 reuse of both panels.
+FER_DEV void tile_of(int bid, int tiles_m, int tiles_n, int& tm, int& tn) {
+  const int nwg = tiles_m * tiles_n;
+  int wgid = bid;
+  if (nwg >= 16) {
+    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  }
+  constexpr int GROUP = 8;
+  const int per_group = GROUP * tiles_n;
+  const int g = wgid / per_group;
+  const int first = g * GROUP;
+  const int gsize = min(tiles_m - first, GROUP);
+  const int w = wgid - g * per_group;
+  tm = first + w % gsize;
+  tn = w / gsize;
+}
+
+// ------------------------------------------------------------- LDS-DMA stage
+template <int R, bool KC, int NW>
+FER_DEV void stage_tile(__amdgpu_buffer_rsrc_t rs, char* lds_tile, int wave, int lane, long ld, int r0,
+                        int rmax, int k0, int kmax) {
+  constexpr int NI = R / 8 / NW;  // 1 KiB wave-instructions per wave
+  static_assert(NI * NW * 8 == R, "tile/wave mismatch");
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int gi = wave * NI + i;
+    uint32_t voff;
+    if constexpr (KC) {
+      const int row = gi * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ ((row >> 1) & 7);
+      const int gr = r0 + row, gk = k0 + c * 8;
+      voff = (gr < rmax && gk < kmax) ? (uint32_t)(((long)gr * ld + gk) * 2) : FER_OOB;
+    } else {
+      constexpr int RB = R * 2;
+      const int byte = gi * 1024 + lane * 16;
+      const int k = byte / RB;
+      const int cp = (byte % RB) >> 4;
+      const int rho = (k & 3) | (((k >> 3) & 1) << 2);
+      const int c = cp ^ (rho << 1);
+      const int gk = k0 + k, gc = r0 + c * 8;
+      voff = (gk < kmax && gc < rmax) ? (uint32_t)(((long)gk * ld + gc) * 2) : FER_OOB;
+    }
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(lds_tile + gi * 1024), 16, voff, 0, 0, 0);
+  }
+}
+
+// 16 rows/cols x 32 k fragment: lane l holds index (l&15), k = 8*(l>>4) + j.
+template <int R, bool KC>
+FER_DEV bf16x8 read_frag(const char* lds_tile, int i0, int kk, int lane) {
+  if constexpr (KC) {
+    const int row = i0 + (lane & 15);
+    const int c = (4 * kk + (lane >> 4)) ^ ((row >> 1) & 7);
+    return *(const bf16x8*)(lds_tile + row * 128 + c * 16);
+  } else {
+    constexpr int RB = R * 2;
+    const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+    const int kb = 32 * kk + 8 * g + q;
+    const int c = (i0 >> 3) + (p >> 1);
+    const int k1 = kb, k2 = kb + 4;
+    const int rho1 = (k1 & 3) | (((k1 >> 3) & 1) << 2);
+    const int rho2 = (k2 & 3) | (((k2 >> 3) & 1) << 2);
+    const char* a1 = lds_tile + k1 * RB + ((c ^ (rho1 << 1)) << 4) + (p & 1) * 8;
+    const char* a2 = lds_tile + k2 * RB + ((c ^ (rho2 << 1)) << 4) + (p & 1) * 8;
+    short4_t t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4_t*)a1);
+    short4_t t2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4_t*)a2);
+    bf16x4 b1 = __builtin_bit_cast(bf16x4, t1), b2 = __builtin_bit_cast(bf16x4, t2);
+    return bf16x8{b1[0], b1[1], b1[2], b1[3], b2[0], b2[1], b2[2], b2[3]};
+  }
+}
+
+template <int BM, int BN, int WM, int WN, bool AKC, bool BKC>
+__global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g, EpiArgs e) {
+  constexpr int NW = WM * WN;
+  constexpr int BK = 64;
+  constexpr int TM = BM / WM, TN = BN / WN;
+  constexpr int FM = TM / 16, FN = TN / 16;
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave % WM, wn = wave / WM;
+
+  int tm, tn;
+  tile_of(blockIdx.x, g.tiles_m, g.tiles_n, tm, tn);
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int ks = blockIdx.y;
+  const int kbeg = ks * g.k_chunk;
+  const int kend = min(g.K, kbeg + g.k_chunk);
+  const int nk = (kend - kbeg + BK - 1) / BK;
+
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(g.A);
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(g.B);
+
+  f32x4 acc[FN][FM];
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int j = 0; j < FM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (nk > 0) {
+    stage_tile<BM, AKC, NW>(ra, smem, wave, lane, g.lda, m0, g.M, kbeg, kend);
+    stage_tile<BN, BKC, NW>(rb, smem + A_BYTES, wave, lane, g.ldb, n0, g.N, kbeg, kend);
+  }
+  for (int t = 0; t < nk; ++t) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const char* cur = smem + (t & 1) * STAGE;
+    if (t + 1 < nk) {
+      char* nxt = smem + ((t + 1) & 1) * STAGE;
+      const int k0 = kbeg + (t + 1) * BK;
+      stage_tile<BM, AKC, NW>(ra, nxt, wave, lane, g.lda, m0, g.M, k0, kend);
+      stage_tile<BN, BKC, NW>(rb, nxt + A_BYTES, wave, lane, g.ldb, n0, g.N, k0, kend);
+    }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[FM], bfr[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) af[i] = read_frag<BM, AKC>(cur, wm * TM + i * 16, kk, lane);
+#pragma unroll
+      for (int i = 0; i < FN; ++i) bfr[i] = read_frag<BN, BKC>(cur + A_BYTES, wn * TN + i * 16, kk, lane);
+#pragma unroll
+      for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int j = 0; j < FM; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[i], af[j], acc[i][j], 0, 0, 0);
+    }
+  }
+
+  // ---- epilogue: lane holds C[m][n..n+3]
+  const long mb = m0 + wm * TM + (lane & 15);
+  const long nb = n0 + wn * TN + 4 * (lane >> 4);
+  if (g.partial) {  // split-K partial slab, fp32 [split][M][N]
+    float* ws = g.ws + (long)ks * g.M * g.N;
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+      for (int j = 0; j < FM; ++j) {
+        const long m = mb + j * 16, n = nb + i * 16;
+        if (m < g.M && n < g.N) *(f32x4*)(ws + m * g.N + n) = acc[i][j];
+      }
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int j = 0; j < FM; ++j) {
+      const long m = mb + j * 16, n = nb + i * 16;
+      if (m < g.M && n < g.N) epi4<bf16>(e, m, n, acc[i][j]);
+    }
+}
+
+// Ordered (deterministic) split-K reduction + epilogue.
+template <typename T>
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ ws, int splits, long M, long N,
+                                                           EpiArgs e) {
+  const long n4 = N >> 2;
+  const long total = M * n4;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256L) {
+    const long m = i / n4, n = (i - m * n4) * 4;
+    f32x4 v = *(const f32x4*)(ws + m * N + n);
+    for (int s = 1; s < splits; ++s) v += *(const f32x4*)(ws + (long)s * M * N + m * N + n);
+    epi4<T>(e, m, n, v);
+  }
+}
+
+// fp32 parity path: 64x64 tile, BK 16, 256 threads x (4x4) outputs, exact fp32 FMA.
+__global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs g, EpiArgs e, int akc, int bkc) {
+  __shared__ float As[16][68];
+  __shared__ float Bs[16][68];
+  const int t = threadIdx.x;
+  const int tm = blockIdx.x / g.tiles_n, tn = blockIdx.x % g.tiles_n;
+  const long m0 = tm * 64L, n0 = tn * 64L;
+  const float* A = (const float*)g.A;
+  const float* B = (const float*)g.B;
+  float acc[4][4] = {};
+  const int ty = t >> 4, tx = t & 15;
+  for (int k0 = 0; k0 < g.K; k0 += 16) {
+    for (int i = t; i < 16 * 64; i += 256) {
+      int kk, mm;
+      if (akc) { mm = i >> 4; kk = i & 15; } else { kk = i >> 6; mm = i & 63; }
+      const long m = m0 + mm, k = k0 + kk;
+      As[kk][mm] = (m < g.M && k < g.K) ? (akc ? A[m * g.lda + k] : A[k * g.lda + m]) : 0.f;
+      int nn;
+      if (bkc) { nn = i >> 4; kk = i & 15; } else { kk = i >> 6; nn = i & 63; }
+      const long n = n0 + nn, k2 = k0 + kk;
+      Bs[kk][nn] = (n < g.N && k2 < g.K) ? (bkc ? B[n * g.ldb + k2] : B[k2 * g.ldb + n]) : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk) {
+      float a[4], b[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) { a[r] = As[kk][ty * 4 + r]; b[r] = Bs[kk][tx * 4 + r]; }
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[r][c] = fmaf(a[r], b[c], acc[r][c]);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const long m = m0 + ty * 4 + r, n = n0 + tx * 4;
+    if (m < g.M && n < g.N) epi4<float>(e, m, n, f32x4{acc[r][0], acc[r][1], acc[r][2], acc[r][3]});
+  }
+}
+
+// -------------------------------------------------------------------- launch
+template <int BM, int BN, int WM, int WN, bool AKC, bool BKC>
+static int launch_bf16(GemmArgs g, const EpiArgs& e, hipStream_t st) {
+  g.tiles_m = (g.M + BM - 1) / BM;
+  g.tiles_n = (g.N + BN - 1) / BN;
+  dim3 grid(g.tiles_m * g.tiles_n, g.splits);
+  hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, WM, WN, AKC, BKC>), grid, dim3(64 * WM * WN), 0, st, g, e);
+  return 0;
+}
+
+template <bool AKC, bool BKC>
+static int dispatch_tile(GemmArgs g, const EpiArgs& e, hipStream_t st) {
+  const long t256 = ((g.M + 255) / 256) * ((g.N + 255) / 256) * (long)g.splits;
+  if (t256 >= 200) return launch_bf16<256, 256, 2, 4, AKC, BKC>(g, e, st);
+  return launch_bf16<128, 128, 2, 2, AKC, BKC>(g, e, st);
+}
+
+int gemm_launch(const GemmDesc& d, const EpiArgs& e_in, hipStream_t st) {
+  EpiArgs e = e_in;
+  GemmArgs g{};
+  g.A = d.A; g.B = d.B; g.lda = d.lda; g.ldb = d.ldb;
+  g.M = d.M; g.N = d.N; g.K = d.K;
+  if (d.M <= 0 || d.N <= 0) return 0;
+  if (d.N % 4) return set_error("gemm: N must be a multiple of 4");
+  if (d.dtype == FER_F32) {
+    g.tiles_m = (d.M + 63) / 64;
+    g.tiles_n = (d.N + 63) / 64;
+    g.splits = 1;
+    hipLaunchKernelGGL(gemm_f32_kernel, dim3(g.tiles_m * g.tiles_n), dim3(256), 0, st, g, e, d.a_kc, d.b_kc);
+    return hip_check("gemm_f32");
+  }
+  // bf16: alignment contract of the DMA staging (16-byte chunks)
+  if ((d.a_kc && (d.K % 8 || d.lda % 8)) || (!d.a_kc && (d.M % 8 || d.lda % 8)))
+    return set_error("gemm: A layout needs 8-element aligned rows");
+  if ((d.b_kc && (d.K % 8 || d.ldb % 8)) || (!d.b_kc && (d.N % 8 || d.ldb % 8)))
+    return set_error("gemm: B layout needs 8-element aligned rows");
+  const long a_bytes = (d.a_kc ? (long)(d.M - 1) * d.lda + d.K : (long)(d.K - 1) * d.lda + d.M) * 2;
+  const long b_bytes = (d.b_kc ? (long)(d.N - 1) * d.ldb + d.K : (long)(d.K - 1) * d.ldb + d.N) * 2;
+  if (a_bytes >= 0x7FFFFFF0L || b_bytes >= 0x7FFFFFF0L) return set_error("gemm: operand exceeds 2 GiB");
+
+  // split-K when the output tiles alone cannot fill 256 CUs
+  int splits = 1;
+  const long tiles = ((d.M + 255) / 256) * ((d.N + 255) / 256);
+  const long tiles128 = ((d.M + 127) / 128) * ((d.N + 127) / 128);
+  if (d.ws && tiles < 200 && tiles128 < 256 && d.K >= 1024) {
+    const long t = tiles128;
+    splits = (int)std::min<long>((512 + t - 1) / t, d.K / 256);
+    splits = std::max(1, std::min<int>(splits, (int)(d.ws_bytes / ((long)d.M * d.N * 4))));
+  }
+  g.splits = splits;
+  g.k_chunk = splits > 1 ? (((d.K + splits - 1) / splits + 63) / 64) * 64 : d.K;
+  if (splits > 1) g.splits = (d.K + g.k_chunk - 1) / g.k_chunk;
+  g.partial = g.splits > 1;
+  g.ws = d.ws;
+
+  if (d.a_kc && d.b_kc) dispatch_tile<true, true>(g, e, st);
+  else if (d.a_kc && !d.b_kc) dispatch_tile<true, false>(g, e, st);
+  else if (!d.a_kc && !d.b_kc) dispatch_tile<false, false>(g, e, st);
+  else dispatch_tile<false, true>(g, e, st);
+  int rc = hip_check("gemm_bf16");
+  if (rc || !g.partial) return rc;
+  const long work = (long)d.M * (d.N / 4);
+  const int blocks = (int)std::min<long>((work + 255) / 256, 4096);
+  hipLaunchKernelGGL(splitk_reduce_kernel<bf16>, dim3(blocks), dim3(256), 0, st, d.ws, g.splits, (long)d.M,
+                     (long)d.N, e);
+  return hip_check("splitk_reduce");
+}
+
+}  // namespace fer

@@ -1,0 +1,196 @@
+// LayerNorm forward / backward (HBM-bound, one wave per row, vectorised 4-wide).
+//
+// Post-norm nn.TransformerEncoderLayer (norm1/norm2, eps 1e-5) and timm pre-norm
+// Block (eps 1e-6). Forward saves (mean, rstd) per row. Backward fuses: the
+// residual-gradient add, the dropout-mask application for the branch that fed
+// the norm (post-norm `LN(x + Drop(h))` -> d h = Drop'(d(x+Drop h))), and the
+// per-column partial sums for dgamma, dbeta and the branch bias gradient, reduced
+// afterwards in fixed block order (deterministic).
+#include "common.h"
+#include "fervit_internal.h"
+
+namespace fer {
+
+constexpr int LN_VPL = 4;  // vectors (of 4) per lane: D <= 1024
+
+template <typename T>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, long ldx, const float* __restrict__ g,
+                                                     const float* __restrict__ b, int grows, int rdiv,
+                                                     T* __restrict__ y, long ldy, float* __restrict__ mean,
+                                                     float* __restrict__ rstd, int M, int D, float eps) {
+  const int lane = threadIdx.x & 63;
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const int nv = D >> 2;
+  f32x4 v[LN_VPL];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < LN_VPL; ++i) {
+    const int c = (lane + i * 64);
+    v[i] = c < nv ? load4<T>(x + row * ldx + c * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+    s += v[i][0] + v[i][1] + v[i][2] + v[i][3];
+  }
+  const float mu = wave_sum(s) / D;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < LN_VPL; ++i) {
+    const int c = (lane + i * 64);
+    if (c < nv) {
+      f32x4 d = v[i] - mu;
+      q += d[0] * d[0] + d[1] * d[1] + d[2] * d[2] + d[3] * d[3];
+    }
+  }
+  const float rs = rsqrtf(wave_sum(q) / D + eps);
+  const long gr = grows > 1 ? ((row / rdiv) % grows) * D : 0;
+#pragma unroll
+  for (int i = 0; i < LN_VPL; ++i) {
+    const int c = (lane + i * 64);
+    if (c < nv) {
+      f32x4 gg = *(const f32x4*)(g + gr + c * 4), bb = *(const f32x4*)(b + gr + c * 4);
+      store4<T>(y + row * ldy + c * 4, (v[i] - mu) * rs * gg + bb);
+    }
+  }
+  if (lane == 0) {
+    if (mean) mean[row] = mu;
+    if (rstd) rstd[row] = rs;
+  }
+}
+
+// partial layout: ws[blk][3][D]
+template <typename T>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, long lddy, const T* __restrict__ x,
+                                                     long ldx, const float* __restrict__ mean,
+                                                     const float* __restrict__ rstd, const float* __restrict__ g,
+                                                     int grows, int rdiv, const T* __restrict__ res, long ldr,
+                                                     T* __restrict__ dx, long lddx, T* __restrict__ dxd,
+                                                     uint32_t thr, float dscale, uint64_t seed,
+                                                     float* __restrict__ part, int want_part, int M, int D) {
+  __shared__ float red[4][3][LN_VPL * 256];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int nv = D >> 2;
+  f32x4 pg[LN_VPL], pb[LN_VPL], pd[LN_VPL];
+#pragma unroll
+  for (int i = 0; i < LN_VPL; ++i) pg[i] = pb[i] = pd[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (long row = (long)blockIdx.x * 4 + w; row < M; row += (long)gridDim.x * 4) {
+    const float mu = mean[row], rs = rstd[row];
+    const long gr = grows > 1 ? ((row / rdiv) % grows) * D : 0;
+    f32x4 xh[LN_VPL], gy[LN_VPL], dyv[LN_VPL];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < LN_VPL; ++i) {
+      const int c = lane + i * 64;
+      if (c < nv) {
+        dyv[i] = load4<T>(dy + row * lddy + c * 4);
+        xh[i] = (load4<T>(x + row * ldx + c * 4) - mu) * rs;
+        gy[i] = dyv[i] * *(const f32x4*)(g + gr + c * 4);
+        s1 += gy[i][0] + gy[i][1] + gy[i][2] + gy[i][3];
+        f32x4 t = gy[i] * xh[i];
+        s2 += t[0] + t[1] + t[2] + t[3];
+      } else {
+        dyv[i] = xh[i] = gy[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+    s1 = wave_sum(s1) / D;
+    s2 = wave_sum(s2) / D;
+#pragma unroll
+    for (int i = 0; i < LN_VPL; ++i) {
+      const int c = lane + i * 64;
+      if (c < nv) {
+        f32x4 d = (gy[i] - s1 - xh[i] * s2) * rs;
+        if (res) d += load4<T>(res + row * ldr + c * 4);
+        store4<T>(dx + row * lddx + c * 4, d);
+        if (dxd) {
+          const uint64_t base = (uint64_t)row * (uint64_t)D + (uint64_t)(c * 4);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) d[r] = drop_keep(seed, base + r, thr) ? d[r] * dscale : 0.f;
+          store4<T>(dxd + row * lddx + c * 4, d);
+        }
+        pg[i] += dyv[i] * xh[i];
+        pb[i] += dyv[i];
+        pd[i] += d;
+      }
+    }
+  }
+  if (!want_part) return;
+#pragma unroll
+  for (int i = 0; i < LN_VPL; ++i) {
+    const int c = lane + i * 64;
+    *(f32x4*)&red[w][0][c * 4] = pg[i];
+    *(f32x4*)&red[w][1][c * 4] = pb[i];
+    *(f32x4*)&red[w][2][c * 4] = pd[i];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < 3 * D; c += 256) {
+    const int k = c / D, col = c - k * D;
+    part[(long)blockIdx.x * 3 * D + c] = red[0][k][col] + red[1][k][col] + red[2][k][col] + red[3][k][col];
+  }
+}
+
+// out_k[col] (+)= sum_blk part[blk][k][col] for k in {0,1,2}
+__global__ __launch_bounds__(256) void ln_part_reduce_kernel(const float* __restrict__ part, int nblk, int D,
+                                                             float* o0, float* o1, float* o2, int accumulate) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= 3 * D) return;
+  const int k = c / D, col = c - k * D;
+  float* o = k == 0 ? o0 : (k == 1 ? o1 : o2);
+  if (!o) return;
+  float s = 0.f;
+  for (int b = 0; b < nblk; ++b) s += part[(long)b * 3 * D + c];
+  o[col] = accumulate ? o[col] + s : s;
+}
+
+static int ln_bwd_blocks(int M) { return std::max(1, std::min(ceil_div(M, 4), 512)); }
+
+}  // namespace fer
+
+using namespace fer;
+
+extern "C" int fer_layernorm_fwd(int dtype, const void* x, int64_t ldx, const float* gamma, const float* beta,
+                                 int gamma_rows, int row_div, void* y, int64_t ldy, float* mean, float* rstd, int M,
+                                 int D, float eps, fer_stream_t stream) {
+  if (M <= 0) return 0;
+  if (D % 4 || D > 1024 || ldx % 4 || ldy % 4) return set_error("layernorm_fwd: D must be a multiple of 4 and <= 1024");
+  if (gamma_rows < 1) gamma_rows = 1;
+  if (row_div < 1) row_div = 1;
+  dim3 grid(ceil_div(M, 4));
+  if (dtype == FER_BF16)
+    hipLaunchKernelGGL(ln_fwd_kernel<bf16>, grid, dim3(256), 0, (hipStream_t)stream, (const bf16*)x, (long)ldx, gamma,
+                       beta, gamma_rows, row_div, (bf16*)y, (long)ldy, mean, rstd, M, D, eps);
+  else
+    hipLaunchKernelGGL(ln_fwd_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, (const float*)x, (long)ldx,
+                       gamma, beta, gamma_rows, row_div, (float*)y, (long)ldy, mean, rstd, M, D, eps);
+  return hip_check("layernorm_fwd");
+}
+
+extern "C" int64_t fer_layernorm_bwd_ws(int M, int D) { return (int64_t)ln_bwd_blocks(M) * 3 * D * 4; }
+
+extern "C" int fer_layernorm_bwd(int dtype, const void* dy, int64_t lddy, const void* x, int64_t ldx,
+                                 const float* mean, const float* rstd, const float* gamma, int gamma_rows,
+                                 int row_div, const void* res, int64_t ldr, void* dx, int64_t lddx, void* dx_drop,
+                                 uint32_t drop_thresh, float drop_scale, uint64_t seed, float* dgamma, float* dbeta,
+                                 float* dbias, int accumulate, float* ws, int64_t ws_bytes, int M, int D,
+                                 fer_stream_t stream) {
+  if (M <= 0) return 0;
+  if (D % 4 || D > 1024) return set_error("layernorm_bwd: D must be a multiple of 4 and <= 1024");
+  if (gamma_rows < 1) gamma_rows = 1;
+  if (row_div < 1) row_div = 1;
+  const bool want = dgamma || dbeta || dbias;
+  if (want && gamma_rows != 1) return set_error("layernorm_bwd: parameter grads need shared gamma");
+  const int nblk = ln_bwd_blocks(M);
+  if (want && (!ws || ws_bytes < fer_layernorm_bwd_ws(M, D))) return set_error("layernorm_bwd: workspace too small");
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == FER_BF16)
+    hipLaunchKernelGGL(ln_bwd_kernel<bf16>, dim3(nblk), dim3(256), 0, st, (const bf16*)dy, (long)lddy,
+                       (const bf16*)x, (long)ldx, mean, rstd, gamma, gamma_rows, row_div, (const bf16*)res, (long)ldr,
+                       (bf16*)dx, (long)lddx, (bf16*)dx_drop, drop_thresh, drop_scale, seed, ws, (int)want, M, D);
+  else
+    hipLaunchKernelGGL(ln_bwd_kernel<float>, dim3(nblk), dim3(256), 0, st, (const float*)dy, (long)lddy,
+                       (const float*)x, (long)ldx, mean, rstd, gamma, gamma_rows, row_div, (const float*)res,
+                       (long)ldr, (float*)dx, (long)lddx, (float*)dx_drop, drop_thresh, drop_scale, seed, ws,
+                       (int)want, M, D);
+  int rc = hip_check("layernorm_bwd");
+  if (rc || !want) return rc;
+  hipLaunchKernelGGL(ln_part_reduce_kernel, dim3(ceil_div(3 * D, 256)), dim3(256), 0, st, ws, nblk, D, dgamma, dbeta,
+                     dbias, accumulate);
+  return hip_check("layernorm_bwd_reduce");
+}

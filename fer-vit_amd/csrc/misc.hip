@@ -1,0 +1,818 @@
+// HBM-bound kernels around the transformer trunk: bias-gradient column sums, patch
+// im2col, token assembly (CLS + pos), classification head (LN + Linear on CLS rows),
+// softmax cross-entropy, the w+ prologue (SemanticPE / LayerWiseNorm / LEAM), the
+// LatentDecomposer projection, casts, dropout and the fused AdamW optimizer.
+// All cross-row reductions are two-pass (per-block partials, then a fixed-order sum),
+// so every result is bitwise reproducible run to run.
+#include "common.h"
+#include "fervit_internal.h"
+
+namespace fer {
+
+// ------------------------------------------------------------------ colsum
+// part[rb][n] = sum over the row chunk rb of x[m][n]
+constexpr int CS_ROWBLK = 256;
+template <typename T>
+__global__ __launch_bounds__(256) void colsum_part_kernel(const T* __restrict__ x, long ldx, int M, int N,
+                                                          float* __restrict__ part, int rows_per_blk) {
+  const int c4 = blockIdx.x * 256 + threadIdx.x;  // vec4 column index
+  if (c4 * 4 >= N) return;
+  const int r0 = blockIdx.y * rows_per_blk, r1 = min(M, r0 + rows_per_blk);
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
+  for (int r = r0; r < r1; ++r) s += load4<T>(x + (long)r * ldx + c4 * 4);
+  *(f32x4*)(part + (long)blockIdx.y * N + c4 * 4) = s;
+}
+__global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restrict__ part, int nblk, int N,
+                                                           float* out, int accumulate, const float* scale) {
+  const int n = blockIdx.x * 256 + threadIdx.x;
+  if (n >= N) return;
+  float s = 0.f;
+  for (int b = 0; b < nblk; ++b) s += part[(long)b * N + n];
+  if (scale) s *= *scale;
+  out[n] = accumulate ? out[n] + s : s;
+}
+static int colsum_nblk(int M) { return std::max(1, std::min(ceil_div(M, 64), CS_ROWBLK)); }
+
+// ------------------------------------------------------------------ im2col
+template <typename T>
+__global__ __launch_bounds__(256) void im2col_kernel(const float* __restrict__ x, int B, int C, int Hh, int Ww, int P,
+                                                     T* __restrict__ cols, long ldc) {
+  const int gh = Hh / P, gw = Ww / P, K = C * P * P;
+  const long total = (long)B * gh * gw * K;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256L) {
+    const int k = i % K;
+    const long tok = i / K;
+    const int gx = tok % gw, gy = (tok / gw) % gh, b = tok / ((long)gw * gh);
+    const int c = k / (P * P), kh = (k / P) % P, kw = k % P;
+    cols[tok * ldc + k] = from_f<T>(x[(((long)b * C + c) * Hh + gy * P + kh) * Ww + gx * P + kw]);
+  }
+}
+
+// ------------------------------------------------------------------ tokens
+template <typename T>
+__global__ __launch_bounds__(256) void tokens_fwd_kernel(const T* __restrict__ emb, const float* __restrict__ cls,
+                                                         const float* __restrict__ pos, T* __restrict__ t, int B,
+                                                         int n, int D, uint32_t thr, float dscale, uint64_t seed) {
+  const int N = n + 1;
+  const long total = (long)B * N * D;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256L) {
+    const int d = i % D;
+    const long row = i / D;
+    const int tk = row % N, b = row / N;
+    float v = tk == 0 ? cls[d] : to_f<T>(emb[((long)b * n + tk - 1) * D + d]);
+    v += pos[(long)tk * D + d];
+    if (thr) v = drop_keep(seed, (uint64_t)i, thr) ? v * dscale : 0.f;
+    t[i] = from_f<T>(v);
+  }
+}
+// dpos partial per b-chunk; demb written directly
+template <typename T>
+__global__ __launch_bounds__(256) void tokens_bwd_kernel(const T* __restrict__ dt, T* __restrict__ demb, int B, int n,
+                                                         int D, uint32_t thr, float dscale, uint64_t seed,
+                                                         float* __restrict__ part, int bchunk) {
+  const int N = n + 1;
+  const long cols = (long)N * D;
+  const long j = blockIdx.x * 256L + threadIdx.x;  // (token, d)
+  if (j >= cols) return;
+  const int tk = j / D;
+  const int b0 = blockIdx.y * bchunk, b1 = min(B, b0 + bchunk);
+  float s = 0.f;
+  for (int b = b0; b < b1; ++b) {
+    const long i = (long)b * cols + j;
+    float g = to_f<T>(dt[i]);
+    if (thr) g = drop_keep(seed, (uint64_t)i, thr) ? g * dscale : 0.f;
+    s += g;
+    if (tk > 0 && demb) demb[((long)b * n + tk - 1) * D + (j % D)] = from_f<T>(g);
+  }
+  part[(long)blockIdx.y * cols + j] = s;
+}
+__global__ void tokens_bwd_final(const float* __restrict__ part, int nchunk, int N, int D, float* dcls, float* dpos,
+                                 int accumulate) {
+  const long j = blockIdx.x * 256L + threadIdx.x;
+  if (j >= (long)N * D) return;
+  float s = 0.f;
+  for (int c = 0; c < nchunk; ++c) s += part[(long)c * N * D + j];
+  if (dpos) dpos[j] = accumulate ? dpos[j] + s : s;
+  if (j < D && dcls) dcls[j] = accumulate ? dcls[j] + s : s;
+}
+
+// ------------------------------------------------------------------ head
+// One block (256 threads) per sample. stats[b] = {mean, rstd}.
+template <typename T>
+__global__ __launch_bounds__(256) void head_fwd_kernel(const T* __restrict__ t, long rs, const float* __restrict__ lw,
+                                                       const float* __restrict__ lb, float eps,
+                                                       const float* __restrict__ W, const float* __restrict__ bias,
+                                                       float* __restrict__ logits, float* __restrict__ stats, int D,
+                                                       int C, uint32_t thr, float dscale, uint64_t seed) {
+  __shared__ float h[1024];
+  __shared__ float red[8];
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const T* x = t + (long)b * rs;
+  float s = 0.f;
+  for (int d = tid; d < D; d += 256) {
+    const float v = to_f<T>(x[d]);
+    h[d] = v;
+    s += v;
+  }
+  s = wave_sum(s);
+  if (lane == 0) red[w] = s;
+  __syncthreads();
+  const float mu = (red[0] + red[1] + red[2] + red[3]) / D;
+  float q = 0.f;
+  for (int d = tid; d < D; d += 256) q += (h[d] - mu) * (h[d] - mu);
+  q = wave_sum(q);
+  __syncthreads();
+  if (lane == 0) red[4 + w] = q;
+  __syncthreads();
+  const float rsd = rsqrtf((red[4] + red[5] + red[6] + red[7]) / D + eps);
+  for (int d = tid; d < D; d += 256) {
+    float v = (h[d] - mu) * rsd * lw[d] + lb[d];
+    if (thr) v = drop_keep(seed, (uint64_t)b * D + d, thr) ? v * dscale : 0.f;
+    h[d] = v;
+  }
+  __syncthreads();
+  for (int c = w; c < C; c += 4) {
+    float a = 0.f;
+    for (int d = lane; d < D; d += 64) a += h[d] * W[(long)c * D + d];
+    a = wave_sum(a);
+    if (lane == 0) logits[(long)b * C + c] = a + bias[c];
+  }
+  if (tid == 0) {
+    stats[2 * b] = mu;
+    stats[2 * b + 1] = rsd;
+  }
+}
+// part[b] = [dW (C*D) | dbias (C) | dln_w (D) | dln_b (D)]
+template <typename T>
+__global__ __launch_bounds__(256) void head_bwd_kernel(const T* __restrict__ t, long rs, const float* __restrict__ lw,
+                                                       const float* __restrict__ lb, const float* __restrict__ W,
+                                                       const float* __restrict__ stats,
+                                                       const float* __restrict__ dlogits, T* __restrict__ dt, int D,
+                                                       int C, uint32_t thr, float dscale, uint64_t seed,
+                                                       float* __restrict__ part) {
+  __shared__ float xh[1024], gh[1024];
+  __shared__ float red[8];
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const T* x = t + (long)b * rs;
+  const float mu = stats[2 * b], rsd = stats[2 * b + 1];
+  const long pstride = (long)C * D + C + 2 * D;
+  float* pp = part + (long)b * pstride;
+  float s1 = 0.f, s2 = 0.f;
+  for (int d = tid; d < D; d += 256) {
+    const float xhat = (to_f<T>(x[d]) - mu) * rsd;
+    float hv = xhat * lw[d] + lb[d];
+    bool keep = true;
+    if (thr) keep = drop_keep(seed, (uint64_t)b * D + d, thr);
+    const float hd = thr ? (keep ? hv * dscale : 0.f) : hv;
+    float g = 0.f;
+    for (int c = 0; c < C; ++c) {
+      const float dl = dlogits[(long)b * C + c];
+      g += dl * W[(long)c * D + d];
+      pp[(long)c * D + d] = dl * hd;
+    }
+    if (thr) g = keep ? g * dscale : 0.f;
+    pp[(long)C * D + C + d] = g * xhat;  // dln_w
+    pp[(long)C * D + C + D + d] = g;     // dln_b
+    const float gg = g * lw[d];
+    xh[d] = xhat;
+    gh[d] = gg;
+    s1 += gg;
+    s2 += gg * xhat;
+  }
+  if (tid < C) pp[(long)C * D + tid] = dlogits[(long)b * C + tid];
+  s1 = wave_sum(s1);
+  s2 = wave_sum(s2);
+  if (lane == 0) {
+    red[w] = s1;
+    red[4 + w] = s2;
+  }
+  __syncthreads();
+  const float m1 = (red[0] + red[1] + red[2] + red[3]) / D, m2 = (red[4] + red[5] + red[6] + red[7]) / D;
+  for (int d = tid; d < D; d += 256) dt[(long)b * rs + d] = from_f<T>((gh[d] - m1 - xh[d] * m2) * rsd);
+}
+__global__ void head_bwd_final(const float* __restrict__ part, int B, int C, int D, float* dW, float* dbias,
+                               float* dlw, float* dlb, int accumulate) {
+  const long pstride = (long)C * D + C + 2 * D;
+  const long j = blockIdx.x * 256L + threadIdx.x;
+  if (j >= pstride) return;
+  float s = 0.f;
+  for (int b = 0; b < B; ++b) s += part[(long)b * pstride + j];
+  float* o;
+  long k;
+  if (j < (long)C * D) { o = dW; k = j; }
+  else if (j < (long)C * D + C) { o = dbias; k = j - (long)C * D; }
+  else if (j < (long)C * D + C + D) { o = dlw; k = j - (long)C * D - C; }
+  else { o = dlb; k = j - (long)C * D - C - D; }
+  if (!o) return;
+  o[k] = accumulate ? o[k] + s : s;
+}
+template <typename T>
+__global__ void zero_rows_kernel(T* __restrict__ dt, long rows, int D_ld, int D, long stride_keep) {
+  const long total = rows * (long)D;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256L) {
+    const long r = i / D;
+    if (r % stride_keep) dt[r * D_ld + (i % D)] = from_f<T>(0.f);
+  }
+}
+
+// ------------------------------------------------------------------ cross entropy
+__global__ __launch_bounds__(256) void ce_kernel(const float* __restrict__ logits, const int64_t* __restrict__ y,
+                                                 const float* __restrict__ wt, int B, int C, float ls, float gscale,
+                                                 float* loss, float* dlogits) {
+  // single block; pass 1: per-sample terms; pass 2: normalise
+  __shared__ float red[2][4];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  float num = 0.f, den = 0.f;
+  for (int b = tid; b < B; b += 256) {
+    const float* z = logits + (long)b * C;
+    float m = -INFINITY;
+    for (int c = 0; c < C; ++c) m = fmaxf(m, z[c]);
+    float se = 0.f;
+    for (int c = 0; c < C; ++c) se += expf(z[c] - m);
+    const float lse = m + logf(se);
+    const int yb = (int)y[b];
+    const float wy = wt ? wt[yb] : 1.f;
+    float sm = 0.f;
+    for (int c = 0; c < C; ++c) sm += (wt ? wt[c] : 1.f) * (lse - z[c]);
+    num += (1.f - ls) * wy * (lse - z[yb]) + ls / C * sm;
+    den += wy;
+  }
+  num = wave_sum(num);
+  den = wave_sum(den);
+  if (lane == 0) {
+    red[0][w] = num;
+    red[1][w] = den;
+  }
+  __syncthreads();
+  const float N = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+  const float Dn = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+  if (tid == 0 && loss) *loss = N / Dn;
+  if (!dlogits) return;
+  for (int b = tid; b < B; b += 256) {
+    const float* z = logits + (long)b * C;
+    float m = -INFINITY;
+    for (int c = 0; c < C; ++c) m = fmaxf(m, z[c]);
+    float se = 0.f;
+    for (int c = 0; c < C; ++c) se += expf(z[c] - m);
+    const int yb = (int)y[b];
+    const float wy = wt ? wt[yb] : 1.f;
+    float wsum = 0.f;
+    for (int c = 0; c < C; ++c) wsum += wt ? wt[c] : 1.f;
+    for (int c = 0; c < C; ++c) {
+      const float p = expf(z[c] - m) / se;
+      // d/dz_c of (1-ls) wy (lse - z_y) + ls/C sum_k w_k (lse - z_k)
+      float g = (1.f - ls) * wy * (p - (c == yb ? 1.f : 0.f)) + ls / C * (wsum * p - (wt ? wt[c] : 1.f));
+      dlogits[(long)b * C + c] = g * gscale / Dn;
+    }
+  }
+}
+
+// ------------------------------------------------------------------ w+ prologue
+// Block per (row r = b*L + l); 256 threads; D <= 1024. saved[r] = {mean, rstd}.
+__global__ __launch_bounds__(256) void wplus_fwd_kernel(const float* __restrict__ x, float* __restrict__ y, int L,
+                                                        int D, const float* sg, const float* sl, const int64_t* grp,
+                                                        const float* lw, const float* lb, const float* gate,
+                                                        const float* lm, float eps, float* saved) {
+  __shared__ float red[8];
+  const long r = blockIdx.x;
+  const int l = r % L, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  float v[4];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int d = tid + i * 256;
+    float a = 0.f;
+    if (d < D) {
+      a = x[r * D + d];
+      if (sg) a += sg[grp[l] * D + d] + sl[(long)l * D + d];
+    }
+    v[i] = a;
+    s += a;
+  }
+  float mu = 0.f, rs = 0.f;
+  if (lw) {
+    s = wave_sum(s);
+    if (lane == 0) red[w] = s;
+    __syncthreads();
+    mu = (red[0] + red[1] + red[2] + red[3]) / D;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (tid + i * 256 < D) q += (v[i] - mu) * (v[i] - mu);
+    q = wave_sum(q);
+    if (lane == 0) red[4 + w] = q;
+    __syncthreads();
+    rs = rsqrtf((red[4] + red[5] + red[6] + red[7]) / D + eps);
+  }
+  const float sgate = gate ? 1.f / (1.f + __expf(-gate[l])) : 0.f;
+  const float slm = lm ? 1.f / (1.f + __expf(-lm[l])) : 1.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int d = tid + i * 256;
+    if (d >= D) continue;
+    float u = v[i];
+    if (lw) {
+      const float n = (v[i] - mu) * rs * lw[(long)l * D + d] + lb[(long)l * D + d];
+      u = gate ? v[i] + sgate * (n - v[i]) : n;
+    }
+    y[r * D + d] = u * slm;
+  }
+  if (tid == 0 && saved) {
+    saved[2 * r] = mu;
+    saved[2 * r + 1] = rs;
+  }
+}
+// Block per (l, b-chunk). part layout per (chunk, l): [dlw D | dlb D | dsl D | dgate 1 | dleam 1]
+__global__ __launch_bounds__(256) void wplus_bwd_kernel(const float* __restrict__ x, const float* __restrict__ saved,
+                                                        const float* __restrict__ dy, float* __restrict__ dx, int B,
+                                                        int L, int D, int bchunk, const float* sg, const float* sl,
+                                                        const int64_t* grp, const float* lw, const float* lb,
+                                                        const float* gate, const float* lm,
+                                                        float* __restrict__ part) {
+  __shared__ float red[3][4];
+  const int l = blockIdx.x, ch = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int b0 = ch * bchunk, b1 = min(B, b0 + bchunk);
+  const float sgate = gate ? 1.f / (1.f + __expf(-gate[l])) : 0.f;
+  const float slm = lm ? 1.f / (1.f + __expf(-lm[l])) : 1.f;
+  float plw[4] = {}, plb[4] = {}, psl[4] = {};
+  float pgate = 0.f, pleam = 0.f;
+  for (int b = b0; b < b1; ++b) {
+    const long r = (long)b * L + l;
+    const float mu = saved ? saved[2 * r] : 0.f, rs = saved ? saved[2 * r + 1] : 0.f;
+    float v[4], xh[4], n[4], du[4];
+    float a1 = 0.f, a2 = 0.f, ag = 0.f, al = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int d = tid + i * 256;
+      v[i] = xh[i] = n[i] = du[i] = 0.f;
+      if (d >= D) continue;
+      float a = x[r * D + d];
+      if (sg) a += sg[grp[l] * D + d] + sl[(long)l * D + d];
+      v[i] = a;
+      float u = a;
+      if (lw) {
+        xh[i] = (a - mu) * rs;
+        n[i] = xh[i] * lw[(long)l * D + d] + lb[(long)l * D + d];
+        u = gate ? a + sgate * (n[i] - a) : n[i];
+      }
+      const float g = dy[r * D + d];
+      al += g * u;
+      du[i] = g * slm;
+    }
+    // through LWN
+    float dv[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int d = tid + i * 256;
+      dv[i] = du[i];
+      if (d >= D || !lw) continue;
+      const float dn = gate ? du[i] * sgate : du[i];
+      if (gate) {
+        ag += du[i] * (n[i] - v[i]);
+        dv[i] = du[i] * (1.f - sgate);
+      } else {
+        dv[i] = 0.f;
+      }
+      plw[i] += dn * xh[i];
+      plb[i] += dn;
+      const float gg = dn * lw[(long)l * D + d];
+      n[i] = gg;  // reuse: g*gamma
+      a1 += gg;
+      a2 += gg * xh[i];
+    }
+    if (lw) {
+      a1 = wave_sum(a1);
+      a2 = wave_sum(a2);
+      ag = wave_sum(ag);
+      __syncthreads();
+      if (lane == 0) {
+        red[0][w] = a1;
+        red[1][w] = a2;
+        red[2][w] = ag;
+      }
+      __syncthreads();
+      const float m1 = (red[0][0] + red[0][1] + red[0][2] + red[0][3]) / D;
+      const float m2 = (red[1][0] + red[1][1] + red[1][2] + red[1][3]) / D;
+      if (tid == 0) pgate += red[2][0] + red[2][1] + red[2][2] + red[2][3];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (tid + i * 256 < D) dv[i] += (n[i] - m1 - xh[i] * m2) * rs;
+    }
+    al = wave_sum(al);
+    __syncthreads();
+    if (lane == 0) red[0][w] = al;
+    __syncthreads();
+    if (tid == 0) pleam += red[0][0] + red[0][1] + red[0][2] + red[0][3];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int d = tid + i * 256;
+      if (d >= D) continue;
+      dx[r * D + d] = dv[i];
+      psl[i] += dv[i];
+    }
+  }
+  const long ps = 3L * D + 2;
+  float* pp = part + ((long)ch * L + l) * ps;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int d = tid + i * 256;
+    if (d >= D) continue;
+    pp[d] = plw[i];
+    pp[D + d] = plb[i];
+    pp[2 * D + d] = psl[i];
+  }
+  if (tid == 0) {
+    pp[3 * D] = pgate * sgate * (1.f - sgate);
+    pp[3 * D + 1] = pleam * slm * (1.f - slm);
+  }
+}
+// reduce chunks; group embedding grad = sum of layer-embedding grads over its layers
+__global__ void wplus_bwd_final(const float* __restrict__ part, int nch, int L, int D, const int64_t* grp, float* dsg,
+                                float* dsl, float* dlw, float* dlb, float* dgate, float* dleam, int accumulate) {
+  const long ps = 3L * D + 2;
+  const long j = blockIdx.x * 256L + threadIdx.x;
+  if (j >= (long)L * ps) return;
+  const int l = j / ps;
+  const long k = j - (long)l * ps;
+  float s = 0.f;
+  for (int c = 0; c < nch; ++c) s += part[((long)c * L + l) * ps + k];
+  float* o = nullptr;
+  long oi = 0;
+  if (k < D) { o = dlw; oi = (long)l * D + k; }
+  else if (k < 2 * D) { o = dlb; oi = (long)l * D + k - D; }
+  else if (k < 3 * D) { o = dsl; oi = (long)l * D + k - 2 * D; }
+  else if (k == 3 * D) { o = dgate; oi = l; }
+  else { o = dleam; oi = l; }
+  if (o) o[oi] = accumulate ? o[oi] + s : s;
+  if (k >= 2 * D && k < 3 * D && dsg && l == 0) {
+    // group sums computed by the l == 0 thread of each column: fixed order over layers
+    const int d = k - 2 * D;
+    float gsum[3] = {0.f, 0.f, 0.f};
+    for (int ll = 0; ll < L; ++ll) {
+      float t = 0.f;
+      for (int c = 0; c < nch; ++c) t += part[((long)c * L + ll) * ps + 2 * D + d];
+      gsum[grp[ll]] += t;
+    }
+    for (int g = 0; g < 3; ++g) dsg[(long)g * D + d] = accumulate ? dsg[(long)g * D + d] + gsum[g] : gsum[g];
+  }
+}
+
+// ------------------------------------------------------------------ decomposer
+__global__ __launch_bounds__(256) void decomp_scores_kernel(const float* __restrict__ w, const float* __restrict__ dirs,
+                                                            int C, int LD, float* __restrict__ scores) {
+  __shared__ float red[16][4];
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  float acc[16] = {};
+  for (int i = tid; i < LD; i += 256) {
+    const float x = w[(long)b * LD + i];
+    for (int c = 0; c < C; ++c) acc[c] += x * dirs[(long)c * LD + i];
+  }
+  for (int c = 0; c < C; ++c) {
+    const float s = wave_sum(acc[c]);
+    if (lane == 0) red[c][wv] = s;
+  }
+  __syncthreads();
+  if (tid < C) scores[(long)b * C + tid] = red[tid][0] + red[tid][1] + red[tid][2] + red[tid][3];
+}
+__global__ __launch_bounds__(256) void decomp_out_kernel(const float* __restrict__ w, const float* __restrict__ dirs,
+                                                         const float* __restrict__ scores, int C, int LD, int omode,
+                                                         float alpha, int dmode, float* __restrict__ y) {
+  const int b = blockIdx.y;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= LD) return;
+  const float* sc = scores + (long)b * C;
+  float e = 0.f;
+  if (dmode == 0) {
+    for (int c = 0; c < C; ++c) e += sc[c] * dirs[(long)c * LD + i];
+  } else {
+    int best = 0;
+    float bv = fabsf(sc[0]);
+    for (int c = 1; c < C; ++c)
+      if (fabsf(sc[c]) > bv) { bv = fabsf(sc[c]); best = c; }
+    e = sc[best] * dirs[(long)best * LD + i];
+  }
+  const float x = w[(long)b * LD + i];
+  const float idv = x - e;
+  if (omode == 3) {
+    y[(long)b * 2 * LD + i] = e;
+    y[(long)b * 2 * LD + LD + i] = idv;
+  } else {
+    y[(long)b * LD + i] = omode == 0 ? e : (omode == 1 ? idv : idv + alpha * e);
+  }
+}
+
+// ------------------------------------------------------------------ elementwise
+__global__ void cast_f32_bf16_kernel(const float* __restrict__ x, bf16* __restrict__ y, long n) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256L) y[i] = (bf16)x[i];
+}
+__global__ void cast_bf16_f32_kernel(const bf16* __restrict__ x, float* __restrict__ y, long n) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256L) y[i] = (float)x[i];
+}
+template <typename T>
+__global__ void axpy_kernel(const T* __restrict__ x, const T* __restrict__ t, const float* __restrict__ s,
+                            T* __restrict__ y, long n) {
+  const float a = *s;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256L)
+    y[i] = from_f<T>(to_f<T>(x[i]) + a * to_f<T>(t[i]));
+}
+template <typename T>
+__global__ __launch_bounds__(256) void dot_part_kernel(const T* __restrict__ a, const T* __restrict__ b, long n,
+                                                       float* __restrict__ part) {
+  __shared__ float red[4];
+  float s = 0.f;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256L)
+    s += to_f<T>(a[i]) * (b ? to_f<T>(b[i]) : to_f<T>(a[i]));
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+__global__ void sum_final_kernel(const float* __restrict__ part, int n, float* out, int accumulate) {
+  if (threadIdx.x) return;
+  float s = 0.f;
+  for (int i = 0; i < n; ++i) s += part[i];
+  *out = accumulate ? *out + s : s;
+}
+template <typename T>
+__global__ void dropout_kernel(const T* __restrict__ x, T* __restrict__ y, long n, uint32_t thr, float sc,
+                               uint64_t seed) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256L)
+    y[i] = from_f<T>(drop_keep(seed, (uint64_t)i, thr) ? to_f<T>(x[i]) * sc : 0.f);
+}
+__global__ void clip_coef_kernel(const float* sumsq, float sq_scale, float max_norm, float* coef) {
+  if (threadIdx.x) return;
+  const float nrm = sqrtf(*sumsq * sq_scale);
+  *coef = fminf(1.f, max_norm / (nrm + 1e-6f));
+}
+
+// ------------------------------------------------------------------ AdamW
+__global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                    float* __restrict__ m, float* __restrict__ v, bf16* __restrict__ pb,
+                                                    const fer_adamw_segment* __restrict__ segs, float gscale,
+                                                    const float* __restrict__ clip) {
+  const fer_adamw_segment sg = segs[blockIdx.y];
+  const float sc = gscale * (clip ? *clip : 1.f);
+  const float bc1 = 1.f - powf(sg.beta1, (float)sg.step);
+  const float bc2 = 1.f - powf(sg.beta2, (float)sg.step);
+  const float step_size = sg.lr / bc1;
+  const float bc2s = sqrtf(bc2);
+  const float decay = 1.f - sg.lr * sg.weight_decay;
+  for (long j = blockIdx.x * 256L + threadIdx.x; j < sg.numel; j += (long)gridDim.x * 256L) {
+    const long i = sg.offset + j;
+    const float gr = g[i] * sc;
+    float pv = p[i] * decay;
+    const float mv = sg.beta1 * m[i] + (1.f - sg.beta1) * gr;
+    const float vv = sg.beta2 * v[i] + (1.f - sg.beta2) * gr * gr;
+    m[i] = mv;
+    v[i] = vv;
+    pv -= step_size * mv / (sqrtf(vv) / bc2s + sg.eps);
+    p[i] = pv;
+    if (pb) pb[i] = (bf16)pv;
+  }
+}
+
+static int grid_for(long n) { return (int)std::max<long>(1, std::min<long>((n + 255) / 256, 8192)); }
+
+}  // namespace fer
+
+using namespace fer;
+
+extern "C" int64_t fer_colsum_ws(int M, int N) { return (int64_t)colsum_nblk(M) * N * 4; }
+
+extern "C" int fer_colsum(int dtype, const void* x, int64_t ldx, int M, int N, float* out, int accumulate,
+                          const float* scale_ptr, float* ws, int64_t ws_bytes, fer_stream_t stream) {
+  if (N <= 0) return 0;
+  if (N % 4 || ldx % 4) return set_error("colsum: N and ld must be multiples of 4");
+  const int nblk = colsum_nblk(M);
+  if (!ws || ws_bytes < fer_colsum_ws(M, N)) return set_error("colsum: workspace too small");
+  const int rpb = ceil_div(std::max(M, 1), nblk);
+  hipStream_t st = (hipStream_t)stream;
+  dim3 grid(ceil_div(N / 4, 256), nblk);
+  if (dtype == FER_BF16)
+    hipLaunchKernelGGL(colsum_part_kernel<bf16>, grid, dim3(256), 0, st, (const bf16*)x, (long)ldx, M, N, ws, rpb);
+  else
+    hipLaunchKernelGGL(colsum_part_kernel<float>, grid, dim3(256), 0, st, (const float*)x, (long)ldx, M, N, ws, rpb);
+  hipLaunchKernelGGL(colsum_final_kernel, dim3(ceil_div(N, 256)), dim3(256), 0, st, ws, nblk, N, out, accumulate,
+                     scale_ptr);
+  return hip_check("colsum");
+}
+
+extern "C" int fer_im2col_patch(int dtype, const float* x, int B, int C, int Hh, int Ww, int P, void* cols,
+                                int64_t ldc, fer_stream_t stream) {
+  const long total = (long)B * (Hh / P) * (Ww / P) * C * P * P;
+  if (total <= 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == FER_BF16)
+    hipLaunchKernelGGL(im2col_kernel<bf16>, dim3(grid_for(total)), dim3(256), 0, st, x, B, C, Hh, Ww, P, (bf16*)cols,
+                       (long)ldc);
+  else
+    hipLaunchKernelGGL(im2col_kernel<float>, dim3(grid_for(total)), dim3(256), 0, st, x, B, C, Hh, Ww, P,
+                       (float*)cols, (long)ldc);
+  return hip_check("im2col_patch");
+}
+
+extern "C" int fer_tokens_fwd(int dtype, const void* emb, const float* cls, const float* pos, void* t, int B, int n,
+                              int D, uint32_t drop_thresh, float drop_scale, uint64_t seed, fer_stream_t stream) {
+  const long total = (long)B * (n + 1) * D;
+  if (total <= 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == FER_BF16)
+    hipLaunchKernelGGL(tokens_fwd_kernel<bf16>, dim3(grid_for(total)), dim3(256), 0, st, (const bf16*)emb, cls, pos,
+                       (bf16*)t, B, n, D, drop_thresh, drop_scale, seed);
+  else
+    hipLaunchKernelGGL(tokens_fwd_kernel<float>, dim3(grid_for(total)), dim3(256), 0, st, (const float*)emb, cls,
+                       pos, (float*)t, B, n, D, drop_thresh, drop_scale, seed);
+  return hip_check("tokens_fwd");
+}
+
+static int tokens_chunks(int B) { return std::max(1, std::min(B, 64)); }
+extern "C" int64_t fer_tokens_bwd_ws(int B, int N, int D) { return (int64_t)tokens_chunks(B) * N * D * 4; }
+
+extern "C" int fer_tokens_bwd(int dtype, const void* dt, void* demb, float* dcls, float* dpos, int accumulate, int B,
+                              int n, int D, uint32_t drop_thresh, float drop_scale, uint64_t seed, float* ws,
+                              int64_t ws_bytes, fer_stream_t stream) {
+  const int N = n + 1;
+  if (B <= 0) return 0;
+  const int nch = tokens_chunks(B);
+  if (!ws || ws_bytes < fer_tokens_bwd_ws(B, N, D)) return set_error("tokens_bwd: workspace too small");
+  const int bchunk = ceil_div(B, nch);
+  hipStream_t st = (hipStream_t)stream;
+  dim3 grid(ceil_div((long)N * D, 256), nch);
+  if (dtype == FER_BF16)
+    hipLaunchKernelGGL(tokens_bwd_kernel<bf16>, grid, dim3(256), 0, st, (const bf16*)dt, (bf16*)demb, B, n, D,
+                       drop_thresh, drop_scale, seed, ws, bchunk);
+  else
+    hipLaunchKernelGGL(tokens_bwd_kernel<float>, grid, dim3(256), 0, st, (const float*)dt, (float*)demb, B, n, D,
+                       drop_thresh, drop_scale, seed, ws, bchunk);
+  hipLaunchKernelGGL(tokens_bwd_final, dim3(ceil_div((long)N * D, 256)), dim3(256), 0, st, ws, nch, N, D, dcls, dpos,
+                     accumulate);
+  return hip_check("tokens_bwd");
+}
+
+extern "C" int fer_head_fwd(int dtype, const void* t, int64_t row_stride, const float* ln_w, const float* ln_b,
+                            float eps, const float* W, const float* bias, float* logits, float* stats, int B, int D,
+                            int C, uint32_t drop_thresh, float drop_scale, uint64_t seed, fer_stream_t stream) {
+  if (B <= 0) return 0;
+  if (D > 1024) return set_error("head_fwd: D <= 1024");
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == FER_BF16)
+    hipLaunchKernelGGL(head_fwd_kernel<bf16>, dim3(B), dim3(256), 0, st, (const bf16*)t, (long)row_stride, ln_w, ln_b,
+                       eps, W, bias, logits, stats, D, C, drop_thresh, drop_scale, seed);
+  else
+    hipLaunchKernelGGL(head_fwd_kernel<float>, dim3(B), dim3(256), 0, st, (const float*)t, (long)row_stride, ln_w,
+                       ln_b, eps, W, bias, logits, stats, D, C, drop_thresh, drop_scale, seed);
+  return hip_check("head_fwd");
+}
+
+extern "C" int64_t fer_head_bwd_ws(int B, int D, int C) { return (int64_t)B * ((int64_t)C * D + C + 2 * D) * 4; }
+
+extern "C" int fer_head_bwd(int dtype, const void* t, int64_t row_stride, const float* ln_w, const float* ln_b,
+                            const float* W, const float* stats, const float* dlogits, void* dt, int zero_rest,
+                            int rows_total, int D_ld, float* dln_w, float* dln_b, float* dW, float* dbias,
+                            int accumulate, int B, int D, int C, uint32_t drop_thresh, float drop_scale,
+                            uint64_t seed, float* ws, int64_t ws_bytes, fer_stream_t stream) {
+  if (B <= 0) return 0;
+  if (D > 1024) return set_error("head_bwd: D <= 1024");
+  if (!ws || ws_bytes < fer_head_bwd_ws(B, D, C)) return set_error("head_bwd: workspace too small");
+  hipStream_t st = (hipStream_t)stream;
+  if (zero_rest) {
+    const long total = (long)rows_total * D;
+    if (dtype == FER_BF16)
+      hipLaunchKernelGGL(zero_rows_kernel<bf16>, dim3(grid_for(total)), dim3(256), 0, st, (bf16*)dt, (long)rows_total,
+                         D_ld, D, (long)(row_stride / D_ld));
+    else
+      hipLaunchKernelGGL(zero_rows_kernel<float>, dim3(grid_for(total)), dim3(256), 0, st, (float*)dt,
+                         (long)rows_total, D_ld, D, (long)(row_stride / D_ld));
+  }
+  if (dtype == FER_BF16)
+    hipLaunchKernelGGL(head_bwd_kernel<bf16>, dim3(B), dim3(256), 0, st, (const bf16*)t, (long)row_stride, ln_w, ln_b,
+                       W, stats, dlogits, (bf16*)dt, D, C, drop_thresh, drop_scale, seed, ws);
+  else
+    hipLaunchKernelGGL(head_bwd_kernel<float>, dim3(B), dim3(256), 0, st, (const float*)t, (long)row_stride, ln_w,
+                       ln_b, W, stats, dlogits, (float*)dt, D, C, drop_thresh, drop_scale, seed, ws);
+  const long ps = (long)C * D + C + 2 * D;
+  hipLaunchKernelGGL(head_bwd_final, dim3(ceil_div(ps, 256)), dim3(256), 0, st, ws, B, C, D, dW, dbias, dln_w, dln_b,
+                     accumulate);
+  return hip_check("head_bwd");
+}
+
+extern "C" int fer_cross_entropy(const float* logits, const int64_t* labels, const float* weight, int B, int C,
+                                 float label_smoothing, float grad_scale, float* loss, float* dlogits,
+                                 fer_stream_t stream) {
+  if (B <= 0) return 0;
+  hipLaunchKernelGGL(ce_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, logits, labels, weight, B, C,
+                     label_smoothing, grad_scale, loss, dlogits);
+  return hip_check("cross_entropy");
+}
+
+static int wplus_chunks(int B) { return std::max(1, std::min(B, 32)); }
+extern "C" int64_t fer_wplus_ws(int B, int L, int D) { return (int64_t)wplus_chunks(B) * L * (3L * D + 2) * 4; }
+
+extern "C" int fer_wplus_fwd(const float* x, float* y, int B, int L, int D, const float* spe_group,
+                             const float* spe_layer, const int64_t* groups, const float* lwn_w, const float* lwn_b,
+                             const float* lwn_gate, const float* leam_w, float eps, float* saved,
+                             fer_stream_t stream) {
+  if (B <= 0) return 0;
+  if (D > 1024) return set_error("wplus_fwd: D <= 1024");
+  hipLaunchKernelGGL(wplus_fwd_kernel, dim3(B * L), dim3(256), 0, (hipStream_t)stream, x, y, L, D, spe_group,
+                     spe_layer, groups, lwn_w, lwn_b, lwn_gate, leam_w, eps, saved);
+  return hip_check("wplus_fwd");
+}
+
+extern "C" int fer_wplus_bwd(const float* x, const float* saved, const float* dy, float* dx, int B, int L, int D,
+                             const float* spe_group, const float* spe_layer, const int64_t* groups,
+                             const float* lwn_w, const float* lwn_b, const float* lwn_gate, const float* leam_w,
+                             float eps, float* d_spe_group, float* d_spe_layer, float* d_lwn_w, float* d_lwn_b,
+                             float* d_lwn_gate, float* d_leam_w, int accumulate, float* ws, int64_t ws_bytes,
+                             fer_stream_t stream) {
+  (void)eps;
+  if (B <= 0) return 0;
+  if (!ws || ws_bytes < fer_wplus_ws(B, L, D)) return set_error("wplus_bwd: workspace too small");
+  const int nch = wplus_chunks(B);
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(wplus_bwd_kernel, dim3(L, nch), dim3(256), 0, st, x, saved, dy, dx, B, L, D, ceil_div(B, nch),
+                     spe_group, spe_layer, groups, lwn_w, lwn_b, lwn_gate, leam_w, ws);
+  const long tot = (long)L * (3L * D + 2);
+  hipLaunchKernelGGL(wplus_bwd_final, dim3(ceil_div(tot, 256)), dim3(256), 0, st, ws, nch, L, D, groups, d_spe_group,
+                     d_spe_layer, d_lwn_w, d_lwn_b, d_lwn_gate, d_leam_w, accumulate);
+  return hip_check("wplus_bwd");
+}
+
+extern "C" int fer_decompose(const float* w, const float* dirs, int B, int C, int LD, int output_mode, float alpha,
+                             int decompose_mode, float* y, float* scores, fer_stream_t stream) {
+  if (B <= 0) return 0;
+  if (C > 16) return set_error("decompose: at most 16 directions");
+  if (!scores) return set_error("decompose: scores buffer required");
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(decomp_scores_kernel, dim3(B), dim3(256), 0, st, w, dirs, C, LD, scores);
+  if (y)
+    hipLaunchKernelGGL(decomp_out_kernel, dim3(ceil_div(LD, 256), B), dim3(256), 0, st, w, dirs, (const float*)scores,
+                       C, LD, output_mode, alpha, decompose_mode, y);
+  return hip_check("decompose");
+}
+
+extern "C" int fer_cast_f32_bf16(const float* x, void* y, int64_t n, fer_stream_t stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(cast_f32_bf16_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, x, (bf16*)y, (long)n);
+  return hip_check("cast_f32_bf16");
+}
+extern "C" int fer_cast_bf16_f32(const void* x, float* y, int64_t n, fer_stream_t stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(cast_bf16_f32_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, (const bf16*)x, y,
+                     (long)n);
+  return hip_check("cast_bf16_f32");
+}
+extern "C" int fer_axpy(int dtype, const void* x, const void* t, const float* scale_ptr, void* y, int64_t n,
+                        fer_stream_t stream) {
+  if (n <= 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == FER_BF16)
+    hipLaunchKernelGGL(axpy_kernel<bf16>, dim3(grid_for(n)), dim3(256), 0, st, (const bf16*)x, (const bf16*)t,
+                       scale_ptr, (bf16*)y, (long)n);
+  else
+    hipLaunchKernelGGL(axpy_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, (const float*)x, (const float*)t,
+                       scale_ptr, (float*)y, (long)n);
+  return hip_check("axpy");
+}
+static int dot_blocks(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>((n + 1023) / 1024, 1024)); }
+extern "C" int fer_dot(int dtype, const void* a, const void* b, int64_t n, float* out, int accumulate, float* ws,
+                       int64_t ws_bytes, fer_stream_t stream) {
+  const int nb = dot_blocks(n);
+  if (!ws || ws_bytes < nb * 4) return set_error("dot: workspace too small");
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == FER_BF16)
+    hipLaunchKernelGGL(dot_part_kernel<bf16>, dim3(nb), dim3(256), 0, st, (const bf16*)a, (const bf16*)b, (long)n, ws);
+  else
+    hipLaunchKernelGGL(dot_part_kernel<float>, dim3(nb), dim3(256), 0, st, (const float*)a, (const float*)b, (long)n,
+                       ws);
+  hipLaunchKernelGGL(sum_final_kernel, dim3(1), dim3(64), 0, st, ws, nb, out, accumulate);
+  return hip_check("dot");
+}
+extern "C" int fer_sumsq(const float* x, int64_t n, float* out, float* ws, int64_t ws_bytes, fer_stream_t stream) {
+  return fer_dot(FER_F32, x, nullptr, n, out, 0, ws, ws_bytes, stream);
+}
+extern "C" int fer_clip_coef(const float* sumsq, float sq_scale, float max_norm, float* coef, fer_stream_t stream) {
+  hipLaunchKernelGGL(clip_coef_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, sumsq, sq_scale, max_norm, coef);
+  return hip_check("clip_coef");
+}
+extern "C" int fer_dropout(int dtype, const void* x, void* y, int64_t n, uint32_t drop_thresh, float drop_scale,
+                           uint64_t seed, fer_stream_t stream) {
+  if (n <= 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == FER_BF16)
+    hipLaunchKernelGGL(dropout_kernel<bf16>, dim3(grid_for(n)), dim3(256), 0, st, (const bf16*)x, (bf16*)y, (long)n,
+                       drop_thresh, drop_scale, seed);
+  else
+    hipLaunchKernelGGL(dropout_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, (const float*)x, (float*)y,
+                       (long)n, drop_thresh, drop_scale, seed);
+  return hip_check("dropout");
+}
+extern "C" int fer_adamw(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, void* param_bf16,
+                         const fer_adamw_segment* segs_device, int nsegs, int64_t max_seg_numel, float grad_scale,
+                         const float* clip_coef, fer_stream_t stream) {
+  if (nsegs <= 0) return 0;
+  dim3 grid((unsigned)std::max<long>(1, std::min<long>((max_seg_numel + 255) / 256, 1024)), nsegs);
+  hipLaunchKernelGGL(adamw_kernel, grid, dim3(256), 0, (hipStream_t)stream, param, grad, exp_avg, exp_avg_sq,
+                     (bf16*)param_bf16, segs_device, grad_scale, clip_coef);
+  return hip_check("adamw");
+}

@@ -1,0 +1,85 @@
+"""FusedAdamW: torch.optim.AdamW semantics (decoupled weight decay, bias correction;
+`train/train_image_vit.py:270-276`) in ONE HIP launch over a model's flat parameter
+buffer, with per-parameter lr / weight_decay from the param groups, optional gradient
+clipping coefficient (clip_grad_norm_, `train_latent_vit_v2.py:133`) computed on device,
+and the bf16 compute copy refreshed in the same pass.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional
+
+import torch
+
+from . import ops
+from ._lib import AdamWSegment, check, lib
+
+
+class FusedAdamW(torch.optim.Optimizer):
+    def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 1e-2,
+                 model=None):
+        defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
+        super().__init__(params, defaults)
+        self.model = model
+        self._flat = None
+        self._m = self._v = None
+        self._segs_dev = None
+        self._seg_key = None
+        self.grad_scale = 1.0        # e.g. 1/world after an all-reduce sum
+        self.clip_coef: Optional[torch.Tensor] = None  # device scalar, consumed by the next step
+
+    def _bind(self):
+        flat = self.model.fer_flat() if self.model is not None else None
+        if flat is None:
+            raise RuntimeError("FusedAdamW needs model= (a fervit FerModule) to locate the flat buffers")
+        if flat is not self._flat:
+            self._flat = flat
+            self._m = torch.zeros_like(flat.data)
+            self._v = torch.zeros_like(flat.data)
+        return flat
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = closure() if closure is not None else None
+        flat = self._bind()
+        segs = []
+        maxn = 0
+        for g in self.param_groups:
+            b1, b2 = g["betas"]
+            for p in g["params"]:
+                if p.grad is None:
+                    continue
+                st = self.state[p]
+                st["step"] = st.get("step", 0) + 1
+                n = p.numel()
+                maxn = max(maxn, n)
+                segs.append((flat.offsets[id(p)], n, g["lr"], g["weight_decay"], b1, b2, g["eps"], st["step"]))
+                if p.grad.data_ptr() != flat.grad_views[id(p)].data_ptr():
+                    flat.grad_views[id(p)].copy_(p.grad)
+        if not segs:
+            return loss
+        arr = (AdamWSegment * len(segs))(*[AdamWSegment(*s) for s in segs])
+        host = torch.frombuffer(bytearray(ctypes.string_at(ctypes.addressof(arr), ctypes.sizeof(arr))),
+                                dtype=torch.uint8)
+        dev = host.to(flat.data.device, non_blocking=False)
+        self._segs_dev = dev
+        half = flat.bf16()
+        check(lib().fer_adamw(flat.data.data_ptr(), flat.grad.data_ptr(), self._m.data_ptr(), self._v.data_ptr(),
+                              half.data_ptr(), dev.data_ptr(), len(segs), maxn, float(self.grad_scale),
+                              ops.ptr(self.clip_coef), ops.stream()), "adamw")
+        flat.mark_half_fresh()
+        self.clip_coef = None
+        return loss
+
+
+def clip_grad_norm_(model, max_norm: float, sq_scale: float = 1.0) -> torch.Tensor:
+    """Device-side clip_grad_norm_ over the model's flat grad buffer: returns the total
+    norm (device scalar) and leaves the clip coefficient for FusedAdamW in
+    `model._fer_clip_coef` (no host synchronisation)."""
+    flat = model.fer_flat()
+    out = torch.empty(2, dtype=torch.float32, device=flat.grad.device)
+    ws = ops.WS.get(4 * 4096, flat.grad.device, slot=3)
+    check(lib().fer_sumsq(flat.grad.data_ptr(), flat.numel, out.data_ptr(), ws.data_ptr(), ws.numel() * 4,
+                          ops.stream()), "sumsq")
+    check(lib().fer_clip_coef(out.data_ptr(), sq_scale, float(max_norm), out[1:].data_ptr(), ops.stream()), "clip")
+    return out

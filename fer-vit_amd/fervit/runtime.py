@@ -1,0 +1,148 @@
+"""Runtime state: precision mode, dropout seed stream, flat parameter storage.
+
+Flat parameter storage (one per model): every parameter of a model lives in ONE
+contiguous fp32 buffer (64-element aligned offsets), its gradient in ONE fp32
+grad buffer with the same offsets, and the bf16 compute copy in ONE bf16 buffer.
+So the optimizer is one fused launch, the bf16 refresh is one cast, and DDP
+all-reduces contiguous buckets of the grad buffer with no packing copies.
+`p.data` / `p.grad` of each nn.Parameter are views into these buffers, so every
+torch API (state_dict, optimizers, clip_grad_norm_) keeps working unchanged.
+"""
+from __future__ import annotations
+
+import os
+import threading
+from typing import Dict, List, Optional
+
+import torch
+
+ALIGN = 64
+
+_state = threading.local()
+
+
+def default_precision() -> str:
+    return os.environ.get("FERVIT_PRECISION", "bf16")
+
+
+class _Seeds:
+    def __init__(self):
+        self.base = None
+        self.counter = 0
+
+    def next(self) -> int:
+        if self.base is None:
+            self.base = (torch.initial_seed() * 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF
+        self.counter += 1
+        z = (self.base + self.counter * 0xBF58476D1CE4E5B9) & 0xFFFFFFFFFFFFFFFF
+        z ^= z >> 31
+        return z
+
+
+SEEDS = _Seeds()
+
+
+def manual_seed(seed: int) -> None:
+    SEEDS.base = (int(seed) * 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF
+    SEEDS.counter = 0
+
+
+def next_seed() -> int:
+    return SEEDS.next()
+
+
+class FlatParams:
+    """Flat fp32 / grad / bf16 storage for a list of parameters (see module doc)."""
+
+    def __init__(self, params: List[torch.nn.Parameter]):
+        self.params = list(params)
+        self.offsets: Dict[int, int] = {}
+        off = 0
+        for p in self.params:
+            self.offsets[id(p)] = off
+            off += (p.numel() + ALIGN - 1) // ALIGN * ALIGN
+        self.numel = max(off, ALIGN)
+        dev = self.params[0].device if self.params else torch.device("cpu")
+        self.device = dev
+        self.data = torch.zeros(self.numel, dtype=torch.float32, device=dev)
+        self.grad = torch.zeros(self.numel, dtype=torch.float32, device=dev)
+        self.half: Optional[torch.Tensor] = None
+        self.half_version = -1
+        with torch.no_grad():
+            for p in self.params:
+                v = self.view(p)
+                v.copy_(p.data)
+                p.data = v
+        self.grad_views = {id(p): self.grad_view(p) for p in self.params}
+
+    def view(self, p, buf=None):
+        buf = self.data if buf is None else buf
+        o = self.offsets[id(p)]
+        return buf[o:o + p.numel()].view(p.shape)
+
+    def grad_view(self, p):
+        return self.view(p, self.grad)
+
+    # ---- bf16 compute copy
+    def bf16(self) -> torch.Tensor:
+        """bf16 shadow of the fp32 buffer, refreshed when any parameter changed in place
+        (version counter of the shared storage) or when marked stale."""
+        from . import ops
+
+        if self.half is None:
+            self.half = torch.empty(self.numel, dtype=torch.bfloat16, device=self.device)
+        v = self.version()
+        if v != self.half_version:
+            ops.cast_bf16(self.data, self.half)
+            self.half_version = v
+        return self.half
+
+    def version(self) -> int:
+        # in-place updates through a Parameter bump that Parameter's own counter
+        # (not the flat base's), so the signature is the sum over parameters.
+        return self.data._version + sum(p._version for p in self.params)
+
+    def mark_half_fresh(self):
+        """Called by the fused optimizer, which refreshes the bf16 copy itself."""
+        self.half_version = self.version()
+
+    def half_view(self, p):
+        return self.view(p, self.bf16())
+
+    # ---- gradient side channel
+    def grad_target(self, p) -> (torch.Tensor, bool):
+        """(view to write p's gradient into, accumulate?) following torch semantics:
+        p.grad None -> overwrite; p.grad is our view -> accumulate; foreign tensor ->
+        copy it into the view, then accumulate."""
+        gv = self.grad_views[id(p)]
+        g = p.grad
+        if g is None:
+            return gv, False
+        if g.data_ptr() == gv.data_ptr():
+            return gv, True
+        with torch.no_grad():
+            gv.copy_(g)
+        return gv, True
+
+    def attach(self, p):
+        gv = self.grad_views[id(p)]
+        if p.grad is None or p.grad.data_ptr() != gv.data_ptr():
+            p.grad = gv
+
+
+_HOOKS: List = []
+
+
+def register_grad_ready_hook(fn) -> None:
+    _HOOKS.append(fn)
+
+
+def remove_grad_ready_hook(fn) -> None:
+    if fn in _HOOKS:
+        _HOOKS.remove(fn)
+
+
+def grads_ready(params) -> None:
+    """Layer backward finished writing these parameters' gradients."""
+    for h in list(_HOOKS):
+        h(params)

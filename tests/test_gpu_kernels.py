@@ -1,0 +1,210 @@
+"""Kernel-level parity on the GPU: every libfervit op vs a plain fp32 torch reference of
+the same op on the same inputs (bf16 path with bf16-appropriate tolerances; the fp32 path
+tight). Dropout masks are rebuilt on the host from the kernel's hash (tests/dropmask.py),
+so dropout paths are checked element-exactly too."""
+import math
+
+import pytest
+import torch
+
+from dropmask import keep_mask
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def ops():
+    from fervit import ops as o
+
+    return o
+
+
+def rel_err(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+def bf(t):
+    return t.to(DEV, torch.bfloat16)
+
+
+# ---------------------------------------------------------------------- GEMM
+GEMM_SHAPES = [(64, 64, 64), (300, 136, 200), (1000, 768, 768), (512, 2304, 768), (4864, 512, 2048),
+               (777, 3072, 776)]
+
+
+@pytest.mark.parametrize("M,N,K", GEMM_SHAPES)
+@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
+def test_linear_fwd_dgrad_wgrad(M, N, K, dtype):
+    o = ops()
+    g = torch.Generator().manual_seed(M * 7 + N)
+    x = torch.randn(M, K, generator=g)
+    w = torch.randn(N, K, generator=g) / math.sqrt(K)
+    dy = torch.randn(M, N, generator=g)
+    cast = bf if dtype == "bf16" else (lambda t: t.to(DEV))
+    xr, wr, dyr = (cast(t).float().cpu().double() for t in (x, w, dy))
+    tol = 1e-2 if dtype == "bf16" else 1e-5
+    y = o.linear_fwd(cast(x), cast(w))
+    assert rel_err(y.cpu(), xr @ wr.t()) < tol
+    dx = o.linear_dgrad(cast(dy), cast(w))
+    assert rel_err(dx.cpu(), dyr @ wr) < tol
+    gw = torch.zeros(N, K, device=DEV)
+    o.linear_wgrad(cast(dy), cast(x), gw)
+    assert rel_err(gw.cpu(), dyr.t() @ xr) < tol
+    o.linear_wgrad(cast(dy), cast(x), gw, accumulate=True)
+    assert rel_err(gw.cpu(), 2 * (dyr.t() @ xr)) < tol
+
+
+@pytest.mark.parametrize("act", ["gelu", "relu"])
+def test_gemm_epilogue_bias_act_dropout_residual(act):
+    o = ops()
+    M, N, K, p, seed = 1030, 640, 384, 0.1, 12345
+    g = torch.Generator().manual_seed(1)
+    x, w = torch.randn(M, K, generator=g), torch.randn(N, K, generator=g) / math.sqrt(K)
+    b, r = torch.randn(N, generator=g), torch.randn(M, N, generator=g)
+    pre = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    y = o.linear_fwd(bf(x), bf(w), b.to(DEV), pre=pre, act=act, dropout=p, seed=seed, res=bf(r))
+    xr, wr, rr = (bf(t).float().cpu() for t in (x, w, r))
+    h = xr @ wr.t() + b
+    a = torch.nn.functional.gelu(h) if act == "gelu" else torch.relu(h)
+    keep = keep_mask(seed, (M, N), p)
+    ref = torch.where(keep, a / (1 - p), torch.zeros(())) + rr
+    assert rel_err(pre.cpu(), h) < 1e-2
+    assert rel_err(y.cpu(), ref) < 1e-2
+    # dgrad through dropout + activation derivative (aux), as in the FFN backward
+    dy = torch.randn(M, K, generator=g)
+    w2 = torch.randn(K, N, generator=g) / math.sqrt(N)  # [out=K, in=N]
+    dF = o.linear_dgrad(bf(dy), bf(w2), dropout=p, seed=seed, drop_ld=N, aux=pre, aux_act=act)
+    dyr, w2r, hr = bf(dy).float().cpu(), bf(w2).float().cpu(), pre.float().cpu()
+    hh = hr.clone().requires_grad_(True)
+    aa = torch.nn.functional.gelu(hh) if act == "gelu" else torch.relu(hh)
+    dG = dyr @ w2r
+    aa.backward(torch.where(keep, dG / (1 - p), torch.zeros(())))
+    assert rel_err(dF.cpu(), hh.grad) < 2e-2
+
+
+def test_gemm_keep_rate():
+    o = ops()
+    M, N, K = 512, 1024, 64
+    x = torch.ones(M, K, device=DEV, dtype=torch.bfloat16)
+    w = torch.full((N, K), 1.0 / K, device=DEV, dtype=torch.bfloat16)
+    y = o.linear_fwd(x, w, dropout=0.1, seed=99).float()
+    frac = (y != 0).float().mean().item()
+    assert abs(frac - 0.9) < 0.005
+    assert torch.allclose(y[y != 0], torch.full_like(y[y != 0], 1 / 0.9), rtol=1e-2)
+
+
+# ---------------------------------------------------------------------- LayerNorm
+@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
+@pytest.mark.parametrize("D", [384, 512, 768])
+def test_layernorm_fwd_bwd(dtype, D):
+    o = ops()
+    M = 1000
+    g = torch.Generator().manual_seed(D)
+    x = torch.randn(M, D, generator=g) * 2 + 0.5
+    w, b = 1 + 0.1 * torch.randn(D, generator=g), 0.1 * torch.randn(D, generator=g)
+    dy, res = torch.randn(M, D, generator=g), torch.randn(M, D, generator=g)
+    cast = bf if dtype == "bf16" else (lambda t: t.to(DEV))
+    tol = 1e-2 if dtype == "bf16" else 1e-5
+    xd = cast(x)
+    mean = torch.empty(M, device=DEV)
+    rstd = torch.empty(M, device=DEV)
+    y = o.layernorm_fwd(xd, w.to(DEV), b.to(DEV), 1e-5, mean=mean, rstd=rstd)
+    xr = xd.float().cpu().requires_grad_(True)
+    wr, br = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    yr = torch.nn.functional.layer_norm(xr, (D,), wr, br, 1e-5)
+    assert rel_err(y.cpu(), yr) < tol
+    p, seed = 0.1, 777
+    dyd = cast(dy)
+    gw = torch.zeros(D, device=DEV)
+    gb = torch.zeros(D, device=DEV)
+    gbias = torch.zeros(D, device=DEV)
+    dxd = torch.empty_like(xd)
+    dx = o.layernorm_bwd(dyd, xd, mean, rstd, w.to(DEV), res=cast(res), dx_drop=dxd, dropout=p, seed=seed, dgamma=gw,
+                         dbeta=gb, dbias=gbias)
+    yr.backward(dyd.float().cpu())
+    dx_ref = xr.grad + cast(res).float().cpu()
+    assert rel_err(dx.cpu(), dx_ref) < tol
+    keep = keep_mask(seed, (M, D), p)
+    dxd_ref = torch.where(keep, dx_ref / (1 - p), torch.zeros(()))
+    assert rel_err(dxd.cpu(), dxd_ref) < tol
+    assert rel_err(gw.cpu(), wr.grad) < 1e-4 + tol
+    assert rel_err(gb.cpu(), br.grad) < 1e-4 + tol
+    assert rel_err(gbias.cpu(), dxd.float().cpu().sum(0)) < 1e-3
+
+
+# ---------------------------------------------------------------------- attention
+def attn_ref(qkv, B, N, H, dh, keep=None, p=0.0):
+    D = H * dh
+    q, k, v = qkv.view(B, N, 3, H, dh).permute(2, 0, 3, 1, 4)
+    s = (q @ k.transpose(-1, -2)) / math.sqrt(dh)
+    P = torch.softmax(s, -1)
+    lse = torch.logsumexp(s, -1)
+    Pd = P if keep is None else torch.where(keep, P / (1 - p), torch.zeros(()))
+    out = (Pd @ v).permute(0, 2, 1, 3).reshape(B * N, D)
+    return out, lse
+
+
+@pytest.mark.parametrize("N,H,dh", [(10, 8, 48), (19, 8, 64), (37, 12, 64), (197, 12, 64), (19, 6, 64)])
+@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_attention_fwd_bwd(N, H, dh, dtype, p):
+    o = ops()
+    B = 3 if N == 197 else 8
+    D = H * dh
+    seed = 4242
+    g = torch.Generator().manual_seed(N * 100 + dh)
+    qkv = torch.randn(B * N, 3 * D, generator=g)
+    dout = torch.randn(B * N, D, generator=g)
+    cast = bf if dtype == "bf16" else (lambda t: t.to(DEV))
+    tol = 2e-2 if dtype == "bf16" else 1e-4
+    qd = cast(qkv)
+    out = torch.empty(B * N, D, device=DEV, dtype=qd.dtype)
+    lse = torch.empty(B * H * N, device=DEV)
+    o.attention_fwd(qd, out, lse, B, N, H, dh, dropout=p, seed=seed)
+    keep = keep_mask(seed, (B, H, N, N), p) if p > 0 else None
+    qr = qd.float().cpu().requires_grad_(True)
+    ref, lse_ref = attn_ref(qr, B, N, H, dh, keep, p)
+    assert rel_err(out.cpu(), ref) < tol
+    assert (lse.cpu() - lse_ref.reshape(-1)).abs().max().item() < (2e-2 if dtype == "bf16" else 1e-4)
+    dd = cast(dout)
+    dqkv = torch.empty_like(qd)
+    o.attention_bwd(qd, out, dd, lse, dqkv, B, N, H, dh, dropout=p, seed=seed)
+    ref.backward(dd.float().cpu())
+    for j, name in enumerate("qkv"):
+        a = dqkv.cpu().float()[:, j * D:(j + 1) * D]
+        b = qr.grad[:, j * D:(j + 1) * D]
+        assert rel_err(a, b) < 2 * tol, name
+
+
+# ---------------------------------------------------------------------- misc
+def test_colsum_and_tokens_and_head():
+    o = ops()
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(3001, 768, generator=g)
+    out = torch.zeros(768, device=DEV)
+    o.colsum(bf(x), out)
+    assert rel_err(out.cpu(), bf(x).float().cpu().sum(0)) < 1e-4
+    B, n, D = 4, 9, 384
+    emb = torch.randn(B * n, D, generator=g)
+    cls, pos = torch.randn(1, 1, D, generator=g), torch.randn(1, n + 1, D, generator=g)
+    t = o.tokens_fwd(emb.to(DEV), cls.to(DEV), pos.to(DEV), B, n, D)
+    ref = torch.cat([cls.expand(B, -1, -1), emb.view(B, n, D)], 1) + pos
+    assert torch.allclose(t.cpu().view(B, n + 1, D), ref, atol=1e-6)
+
+
+def test_cross_entropy_matches_torch():
+    o = ops()
+    g = torch.Generator().manual_seed(9)
+    logits = torch.randn(256, 7, generator=g)
+    y = torch.randint(0, 7, (256,), generator=g)
+    w = torch.rand(7, generator=g) + 0.5
+    for ls in (0.0, 0.1):
+        for wt in (None, w):
+            lg = logits.clone().requires_grad_(True)
+            ref = torch.nn.functional.cross_entropy(lg, y, weight=wt, label_smoothing=ls)
+            ref.backward()
+            loss, dl = o.cross_entropy(logits.to(DEV), y.to(DEV), None if wt is None else wt.to(DEV), ls)
+            assert abs(loss.item() - ref.item()) < 1e-5
+            assert (dl.cpu() - lg.grad).abs().max().item() < 1e-6
