@@ -16,6 +16,9 @@ from ._lib import Epilogue, GemmDesc, check, lib
 
 ACT = {"none": 0, "gelu": 1, "relu": 2}
 
+# Optional callable(desc, launch) used by bench.py to bracket launches with HIP events.
+LAUNCH_PROBE = None
+
 
 def dcode(t: torch.Tensor) -> int:
     if t.dtype == torch.bfloat16:
@@ -106,7 +109,10 @@ def gemm(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, *, a_kc: bool = Tr
     e.ldx = N if aux is None else aux.stride(0)
     e.aux_act = ACT[aux_act]
     e.post_scale = ptr(post_scale)
-    check(lib().fer_gemm(C_ref(d), C_ref(e), stream()), "gemm")
+    if LAUNCH_PROBE is not None:
+        LAUNCH_PROBE(d, lambda: check(lib().fer_gemm(C_ref(d), C_ref(e), stream()), "gemm"))
+    else:
+        check(lib().fer_gemm(C_ref(d), C_ref(e), stream()), "gemm")
     return out
 
 

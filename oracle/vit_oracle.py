@@ -62,15 +62,18 @@ def patch_embed(x: Tensor, w: Tensor, b: Tensor, patch: int) -> Tensor:
     return cols @ w.reshape(w.shape[0], -1).t() + b
 
 
-def attention(q: Tensor, k: Tensor, v: Tensor) -> Tensor:
-    """softmax(q k^T / sqrt(dh)) v per (batch, head); q,k,v [B,H,N,dh]."""
+def attention(q: Tensor, k: Tensor, v: Tensor, p_drop: float = 0.0) -> Tensor:
+    """softmax(q k^T / sqrt(dh)) [dropout] v per (batch, head); q,k,v [B,H,N,dh]."""
     dh = q.shape[-1]
     s = (q @ k.transpose(-1, -2)) / math.sqrt(dh)
     p = torch.softmax(s, dim=-1)
+    if p_drop > 0:
+        p = F.dropout(p, p_drop)
     return p @ v
 
 
-def mha(x: Tensor, w_in: Tensor, b_in: Tensor, w_out: Tensor, b_out: Tensor, heads: int) -> Tensor:
+def mha(x: Tensor, w_in: Tensor, b_in: Tensor, w_out: Tensor, b_out: Tensor, heads: int,
+        p_drop: float = 0.0) -> Tensor:
     """nn.MultiheadAttention self-attention with packed in_proj (rows q|k|v),
     as used by nn.TransformerEncoderLayer (`image_vit.py:101`, `latent_vit.py:24`)."""
     B, N, D = x.shape
@@ -78,24 +81,25 @@ def mha(x: Tensor, w_in: Tensor, b_in: Tensor, w_out: Tensor, b_out: Tensor, hea
     qkv = x @ w_in.t() + b_in
     q, k, v = qkv.split(D, dim=-1)
     sh = lambda t: t.reshape(B, N, heads, dh).permute(0, 2, 1, 3)
-    o = attention(sh(q), sh(k), sh(v)).permute(0, 2, 1, 3).reshape(B, N, D)
+    o = attention(sh(q), sh(k), sh(v), p_drop).permute(0, 2, 1, 3).reshape(B, N, D)
     return o @ w_out.t() + b_out
 
 
 def encoder_layer_postnorm(x: Tensor, p: Dict[str, Tensor], prefix: str, heads: int,
-                           act: str, eps: float = 1e-5) -> Tensor:
-    """nn.TransformerEncoderLayer(norm_first=False), dropout disabled:
-    x = LN1(x + SA(x)); x = LN2(x + W2 act(W1 x + b1) + b2).
-    GELU-erf for ImageViT (`image_vit.py:101-109`), ReLU default for LatentViT
-    (`latent_vit.py:24-30`)."""
+                           act: str, eps: float = 1e-5, p_drop: float = 0.0) -> Tensor:
+    """nn.TransformerEncoderLayer(norm_first=False):
+    x = LN1(x + Drop(SA(x))); x = LN2(x + Drop(W2 Drop(act(W1 x + b1)) + b2)),
+    attention-probability dropout inside SA. GELU-erf for ImageViT (`image_vit.py:101-109`),
+    ReLU default for LatentViT (`latent_vit.py:24-30`). Parity uses p_drop = 0."""
     g = lambda n: p[prefix + n]
+    d = (lambda t: F.dropout(t, p_drop)) if p_drop > 0 else (lambda t: t)
     sa = mha(x, g("self_attn.in_proj_weight"), g("self_attn.in_proj_bias"),
-             g("self_attn.out_proj.weight"), g("self_attn.out_proj.bias"), heads)
-    x = layer_norm(x + sa, g("norm1.weight"), g("norm1.bias"), eps)
+             g("self_attn.out_proj.weight"), g("self_attn.out_proj.bias"), heads, p_drop)
+    x = layer_norm(x + d(sa), g("norm1.weight"), g("norm1.bias"), eps)
     h = x @ g("linear1.weight").t() + g("linear1.bias")
-    h = gelu_erf(h) if act == "gelu" else torch.relu(h)
+    h = d(gelu_erf(h) if act == "gelu" else torch.relu(h))
     ff = h @ g("linear2.weight").t() + g("linear2.bias")
-    return layer_norm(x + ff, g("norm2.weight"), g("norm2.bias"), eps)
+    return layer_norm(x + d(ff), g("norm2.weight"), g("norm2.bias"), eps)
 
 
 def block_prenorm(x: Tensor, p: Dict[str, Tensor], prefix: str, heads: int, eps: float = 1e-6) -> Tensor:
@@ -195,13 +199,16 @@ def cross_entropy(logits: Tensor, labels: Tensor, label_smoothing: float = 0.0,
 
 
 # ------------------------------------------------------------------------ models
-def image_vit_forward(x: Tensor, p: Dict[str, Tensor], patch: int, heads: int, depth: int) -> Tensor:
+def image_vit_forward(x: Tensor, p: Dict[str, Tensor], patch: int, heads: int, depth: int,
+                      p_drop: float = 0.0) -> Tensor:
     """ImageViT.forward (`models_fer_vit/image_vit.py:138-166`)."""
     B = x.shape[0]
     t = patch_embed(x, p["patch_embed.proj.weight"], p["patch_embed.proj.bias"], patch)
     t = torch.cat([p["cls_token"].expand(B, -1, -1), t], 1) + p["pos_embed"]
+    if p_drop > 0:
+        t = F.dropout(t, p_drop)
     for i in range(depth):
-        t = encoder_layer_postnorm(t, p, f"transformer.layers.{i}.", heads, "gelu")
+        t = encoder_layer_postnorm(t, p, f"transformer.layers.{i}.", heads, "gelu", p_drop=p_drop)
     c = layer_norm(t[:, 0], p["norm.weight"], p["norm.bias"], 1e-5)
     return c @ p["head.weight"].t() + p["head.bias"]
 

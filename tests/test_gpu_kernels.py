@@ -131,7 +131,8 @@ def test_layernorm_fwd_bwd(dtype, D):
     assert rel_err(dxd.cpu(), dxd_ref) < tol
     assert rel_err(gw.cpu(), wr.grad) < 1e-4 + tol
     assert rel_err(gb.cpu(), br.grad) < 1e-4 + tol
-    assert rel_err(gbias.cpu(), dxd.float().cpu().sum(0)) < 1e-3
+    # kernel sums the fp32 values before the bf16 rounding of dx_drop
+    assert rel_err(gbias.cpu(), dxd.float().cpu().sum(0)) < (5e-3 if dtype == "bf16" else 1e-5)
 
 
 # ---------------------------------------------------------------------- attention

@@ -72,22 +72,26 @@ def test_eval_logits_and_no_grad():
 
 
 def test_fused_adamw_matches_torch_adamw():
+    """Same gradients into both optimizers (key-bias grads are ~0 by softmax shift
+    invariance, so independent backward passes would differ in their noise)."""
     from fervit.optim import FusedAdamW
 
     m1, _ = build("latent_vit_v2_all")
     m2, _ = build("latent_vit_v2_all")
-    for m in (m1, m2):
-        m.set_precision("fp32")
+    m1.set_precision("fp32")
     o1 = FusedAdamW(m1.parameters(), lr=1e-3, weight_decay=0.05, model=m1)
     o2 = torch.optim.AdamW(m2.parameters(), lr=1e-3, weight_decay=0.05)
     x, y = case_inputs("latent_vit_v2_all")
     for _ in range(3):
-        for m, o in ((m1, o1), (m2, o2)):
-            o.zero_grad()
-            torch.nn.functional.cross_entropy(m(x.cuda()), y.cuda(), label_smoothing=0.1).backward()
-            o.step()
+        o1.zero_grad()
+        o2.zero_grad()
+        torch.nn.functional.cross_entropy(m1(x.cuda()), y.cuda(), label_smoothing=0.1).backward()
+        for a, b in zip(m1.parameters(), m2.parameters()):
+            b.grad = a.grad.detach().clone()
+        o1.step()
+        o2.step()
     for (k, a), (_, b) in zip(m1.named_parameters(), m2.named_parameters()):
-        assert torch.allclose(a, b, atol=1e-5, rtol=1e-4), k
+        assert torch.allclose(a, b, atol=1e-6, rtol=1e-5), k
 
 
 def test_training_reduces_loss_bf16():
