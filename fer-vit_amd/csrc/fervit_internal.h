@@ -24,6 +24,10 @@ struct GemmArgs {
 int set_error(const char* msg);
 int hip_check(const char* what);
 int gemm_launch(const GemmDesc& d, const EpiArgs& e, hipStream_t st);
+inline int ceil_div(long a, long b);
+// out_k[c % seg] (+)= scale * sum_b part[b*ld + c]  (deterministic, misc.hip)
+void part_reduce(const float* part, int nb, long ld, int ncols, int seg, float* o0, float* o1, float* o2,
+                 int accumulate, const float* scale, hipStream_t st);
 
 inline int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
 

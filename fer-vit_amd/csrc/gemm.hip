@@ -9,11 +9,13 @@
 //   dgrad    dX = dY W       : A=dY (KC), B=W (MN)
 //   wgrad    dW = dY^T X     : A=dY (MN), B=X (MN), K = rows = B*N tokens (split-K)
 //
-// bf16 path: v_mfma_f32_16x16x32_bf16 (fp32 accumulate). A and B tiles are staged
-// global->LDS by LDS-DMA (buffer_load ... lds, 16 B/lane) with the swizzle applied on
-// the per-lane SOURCE address (the DMA image is lane-linear):
-//   KC image  [rows][64 k]  (128 B rows): chunk' = chunk ^ ((row>>1)&7)
-//   MN image  [64 k][rows]  (2*R B rows): chunk' = chunk ^ (rho(k)<<1),
+// bf16 path: v_mfma_f32_16x16x32_bf16 (fp32 accumulate), K-step BK = 32, a 4-deep ring of
+// LDS stages filled by LDS-DMA (buffer_load ... lds, 16 B/lane) three K-steps ahead of the
+// MFMAs; each wave waits with a COUNTED vmcnt (only the stage it is about to read) and the
+// stages are handed between waves by a raw s_barrier (no vmcnt(0) drain in the loop).
+// The swizzle is applied on the per-lane SOURCE address (the DMA image is lane-linear):
+//   KC image  [rows][32 k]  (64 B rows):   chunk' = chunk ^ G[(row>>2)&3], G = {0,2,3,1}
+//   MN image  [32 k][rows]  (2*R B rows):  chunk' = chunk ^ (rho(k)<<1),
 //                                          rho(k) = (k&3) | ((k>>3)&1)<<2
 // KC fragments are read with ds_read_b128, MN fragments with two ds_read_b64_tr_b16
 // (hardware transpose); both images are bank-conflict free for their reads.
@@ -37,11 +39,7 @@ FER_DEV void epi4(const EpiArgs& e, long m, long n, f32x4 v) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) v[r] = act_fwd(e.act, v[r]);
   }
-  if (e.drop_thresh) {
-    const uint64_t base = (uint64_t)m * (uint64_t)e.drop_ld + (uint64_t)n;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) v[r] = drop_keep(e.seed, base + r, e.drop_thresh) ? v[r] * e.drop_scale : 0.f;
-  }
+  if (e.drop_thresh) drop4(e.seed, (uint64_t)m * (uint64_t)e.drop_ld + (uint64_t)n, e.drop_thresh, e.drop_scale, v);
   if (e.aux) {
     f32x4 a = load4<T>((const T*)e.aux + m * e.ldx + n);
 #pragma unroll
@@ -80,18 +78,22 @@ FER_DEV void tile_of(int bid, int tiles_m, int tiles_n, int& tm, int& tn) {
 }
 
 // ------------------------------------------------------------- LDS-DMA stage
+constexpr int BK = 32;
+FER_DEV int kc_swz(int row) { return (0x78 >> (2 * ((row >> 2) & 3))) & 3; }
+FER_DEV int mn_rho(int k) { return (k & 3) | (((k >> 3) & 1) << 2); }
+
 template <int R, bool KC, int NW>
 FER_DEV void stage_tile(__amdgpu_buffer_rsrc_t rs, char* lds_tile, int wave, int lane, long ld, int r0,
                         int rmax, int k0, int kmax) {
-  constexpr int NI = R / 8 / NW;  // 1 KiB wave-instructions per wave
-  static_assert(NI * NW * 8 == R, "tile/wave mismatch");
+  constexpr int NI = R * BK * 2 / 1024 / NW;  // 1 KiB wave-instructions per wave
+  static_assert(NI * NW * 1024 == R * BK * 2, "tile/wave mismatch");
 #pragma unroll
   for (int i = 0; i < NI; ++i) {
     const int gi = wave * NI + i;
     uint32_t voff;
     if constexpr (KC) {
-      const int row = gi * 8 + (lane >> 3);
-      const int c = (lane & 7) ^ ((row >> 1) & 7);
+      const int row = gi * 16 + (lane >> 2);
+      const int c = (lane & 3) ^ kc_swz(row);
       const int gr = r0 + row, gk = k0 + c * 8;
       voff = (gr < rmax && gk < kmax) ? (uint32_t)(((long)gr * ld + gk) * 2) : FER_OOB;
     } else {
@@ -99,8 +101,7 @@ FER_DEV void stage_tile(__amdgpu_buffer_rsrc_t rs, char* lds_tile, int wave, int
       const int byte = gi * 1024 + lane * 16;
       const int k = byte / RB;
       const int cp = (byte % RB) >> 4;
-      const int rho = (k & 3) | (((k >> 3) & 1) << 2);
-      const int c = cp ^ (rho << 1);
+      const int c = cp ^ (mn_rho(k) << 1);
       const int gk = k0 + k, gc = r0 + c * 8;
       voff = (gk < kmax && gc < rmax) ? (uint32_t)(((long)gk * ld + gc) * 2) : FER_OOB;
     }
@@ -110,21 +111,18 @@ FER_DEV void stage_tile(__amdgpu_buffer_rsrc_t rs, char* lds_tile, int wave, int
 
 // 16 rows/cols x 32 k fragment: lane l holds index (l&15), k = 8*(l>>4) + j.
 template <int R, bool KC>
-FER_DEV bf16x8 read_frag(const char* lds_tile, int i0, int kk, int lane) {
+FER_DEV bf16x8 read_frag(const char* lds_tile, int i0, int lane) {
   if constexpr (KC) {
     const int row = i0 + (lane & 15);
-    const int c = (4 * kk + (lane >> 4)) ^ ((row >> 1) & 7);
-    return *(const bf16x8*)(lds_tile + row * 128 + c * 16);
+    const int c = (lane >> 4) ^ kc_swz(row);
+    return *(const bf16x8*)(lds_tile + row * 64 + c * 16);
   } else {
     constexpr int RB = R * 2;
     const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
-    const int kb = 32 * kk + 8 * g + q;
+    const int k1 = 8 * g + q, k2 = k1 + 4;
     const int c = (i0 >> 3) + (p >> 1);
-    const int k1 = kb, k2 = kb + 4;
-    const int rho1 = (k1 & 3) | (((k1 >> 3) & 1) << 2);
-    const int rho2 = (k2 & 3) | (((k2 >> 3) & 1) << 2);
-    const char* a1 = lds_tile + k1 * RB + ((c ^ (rho1 << 1)) << 4) + (p & 1) * 8;
-    const char* a2 = lds_tile + k2 * RB + ((c ^ (rho2 << 1)) << 4) + (p & 1) * 8;
+    const char* a1 = lds_tile + k1 * RB + ((c ^ (mn_rho(k1) << 1)) << 4) + (p & 1) * 8;
+    const char* a2 = lds_tile + k2 * RB + ((c ^ (mn_rho(k2) << 1)) << 4) + (p & 1) * 8;
     short4_t t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4_t*)a1);
     short4_t t2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4_t*)a2);
     bf16x4 b1 = __builtin_bit_cast(bf16x4, t1), b2 = __builtin_bit_cast(bf16x4, t2);
@@ -132,15 +130,21 @@ FER_DEV bf16x8 read_frag(const char* lds_tile, int i0, int kk, int lane) {
   }
 }
 
-template <int BM, int BN, int WM, int WN, bool AKC, bool BKC>
+template <int N>
+FER_DEV void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int BM, int BN, int WM, int WN, bool AKC, bool BKC, int STAGES>
 __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g, EpiArgs e) {
   constexpr int NW = WM * WN;
-  constexpr int BK = 64;
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int FM = TM / 16, FN = TN / 16;
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
   constexpr int STAGE = A_BYTES + B_BYTES;
-  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+  constexpr int LPW = STAGE / 1024 / NW;  // LDS-DMA instructions per wave per stage
+  static_assert(STAGES == 4, "vmcnt ladder below assumes a 4-deep ring");
+  __shared__ __attribute__((aligned(1024))) char smem[STAGES * STAGE];
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -163,32 +167,40 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g, 
 #pragma unroll
     for (int j = 0; j < FM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  if (nk > 0) {
-    stage_tile<BM, AKC, NW>(ra, smem, wave, lane, g.lda, m0, g.M, kbeg, kend);
-    stage_tile<BN, BKC, NW>(rb, smem + A_BYTES, wave, lane, g.ldb, n0, g.N, kbeg, kend);
+  // prologue: K-steps 0..STAGES-2 in flight
+#pragma unroll
+  for (int s = 0; s < STAGES - 1; ++s) {
+    if (s < nk) {
+      char* dst = smem + s * STAGE;
+      stage_tile<BM, AKC, NW>(ra, dst, wave, lane, g.lda, m0, g.M, kbeg + s * BK, kend);
+      stage_tile<BN, BKC, NW>(rb, dst + A_BYTES, wave, lane, g.ldb, n0, g.N, kbeg + s * BK, kend);
+    }
   }
   for (int t = 0; t < nk; ++t) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    const char* cur = smem + (t & 1) * STAGE;
-    if (t + 1 < nk) {
-      char* nxt = smem + ((t + 1) & 1) * STAGE;
-      const int k0 = kbeg + (t + 1) * BK;
-      stage_tile<BM, AKC, NW>(ra, nxt, wave, lane, g.lda, m0, g.M, k0, kend);
-      stage_tile<BN, BKC, NW>(rb, nxt + A_BYTES, wave, lane, g.ldb, n0, g.N, k0, kend);
+    // this wave's DMA for K-step t has landed: leave the younger stages in flight
+    const int younger = min(STAGES - 2, nk - 1 - t);
+    if (younger >= 2) wait_vm<2 * LPW>();
+    else if (younger == 1) wait_vm<LPW>();
+    else wait_vm<0>();
+    // every wave's DMA for t landed, and every wave is done reading stage (t-1)
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (t + STAGES - 1 < nk) {
+      char* dst = smem + ((t + STAGES - 1) % STAGES) * STAGE;
+      const int k0 = kbeg + (t + STAGES - 1) * BK;
+      stage_tile<BM, AKC, NW>(ra, dst, wave, lane, g.lda, m0, g.M, k0, kend);
+      stage_tile<BN, BKC, NW>(rb, dst + A_BYTES, wave, lane, g.ldb, n0, g.N, k0, kend);
     }
+    const char* cur = smem + (t % STAGES) * STAGE;
+    bf16x8 af[FM], bfr[FN];
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      bf16x8 af[FM], bfr[FN];
+    for (int i = 0; i < FN; ++i) bfr[i] = read_frag<BN, BKC>(cur + A_BYTES, wn * TN + i * 16, lane);
 #pragma unroll
-      for (int i = 0; i < FM; ++i) af[i] = read_frag<BM, AKC>(cur, wm * TM + i * 16, kk, lane);
+    for (int j = 0; j < FM; ++j) af[j] = read_frag<BM, AKC>(cur, wm * TM + j * 16, lane);
 #pragma unroll
-      for (int i = 0; i < FN; ++i) bfr[i] = read_frag<BN, BKC>(cur + A_BYTES, wn * TN + i * 16, kk, lane);
+    for (int j = 0; j < FM; ++j)
 #pragma unroll
-      for (int i = 0; i < FN; ++i)
-#pragma unroll
-        for (int j = 0; j < FM; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[i], af[j], acc[i][j], 0, 0, 0);
-    }
+      for (int i = 0; i < FN; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[i], af[j], acc[i][j], 0, 0, 0);
   }
 
   // ---- epilogue: lane holds C[m][n..n+3]
@@ -276,7 +288,7 @@ static int launch_bf16(GemmArgs g, const EpiArgs& e, hipStream_t st) {
   g.tiles_m = (g.M + BM - 1) / BM;
   g.tiles_n = (g.N + BN - 1) / BN;
   dim3 grid(g.tiles_m * g.tiles_n, g.splits);
-  hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, WM, WN, AKC, BKC>), grid, dim3(64 * WM * WN), 0, st, g, e);
+  hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, WM, WN, AKC, BKC, 4>), grid, dim3(64 * WM * WN), 0, st, g, e);
   return 0;
 }
 
@@ -320,7 +332,7 @@ int gemm_launch(const GemmDesc& d, const EpiArgs& e_in, hipStream_t st) {
     splits = std::max(1, std::min<int>(splits, (int)(d.ws_bytes / ((long)d.M * d.N * 4))));
   }
   g.splits = splits;
-  g.k_chunk = splits > 1 ? (((d.K + splits - 1) / splits + 63) / 64) * 64 : d.K;
+  g.k_chunk = splits > 1 ? (((d.K + splits - 1) / splits + BK - 1) / BK) * BK : d.K;
   if (splits > 1) g.splits = (d.K + g.k_chunk - 1) / g.k_chunk;
   g.partial = g.splits > 1;
   g.ws = d.ws;

@@ -100,9 +100,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, l
         if (res) d += load4<T>(res + row * ldr + c * 4);
         store4<T>(dx + row * lddx + c * 4, d);
         if (dxd) {
-          const uint64_t base = (uint64_t)row * (uint64_t)D + (uint64_t)(c * 4);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) d[r] = drop_keep(seed, base + r, thr) ? d[r] * dscale : 0.f;
+          drop4(seed, (uint64_t)row * (uint64_t)D + (uint64_t)(c * 4), thr, dscale, d);
           store4<T>(dxd + row * lddx + c * 4, d);
         }
         pg[i] += dyv[i] * xh[i];
@@ -139,7 +137,7 @@ __global__ __launch_bounds__(256) void ln_part_reduce_kernel(const float* __rest
   o[col] = accumulate ? o[col] + s : s;
 }
 
-static int ln_bwd_blocks(int M) { return std::max(1, std::min(ceil_div(M, 4), 512)); }
+static int ln_bwd_blocks(int M) { return std::max(1, std::min(ceil_div(M, 4), 256)); }
 
 }  // namespace fer
 
@@ -190,7 +188,6 @@ extern "C" int fer_layernorm_bwd(int dtype, const void* dy, int64_t lddy, const 
                        (int)want, M, D);
   int rc = hip_check("layernorm_bwd");
   if (rc || !want) return rc;
-  hipLaunchKernelGGL(ln_part_reduce_kernel, dim3(ceil_div(3 * D, 256)), dim3(256), 0, st, ws, nblk, D, dgamma, dbeta,
-                     dbias, accumulate);
+  part_reduce(ws, nblk, 3L * D, 3 * D, D, dgamma, dbeta, dbias, accumulate, nullptr, st);
   return hip_check("layernorm_bwd_reduce");
 }

@@ -9,29 +9,70 @@
 
 namespace fer {
 
+// ------------------------------------------------------------------ reductions
+// Deterministic second pass: out_k[c % seg] (+)= scale * sum_{b<nb} part[b*ld + c],
+// k = c / seg selects one of three outputs. 32 columns x 8 partial-row slices per block,
+// fixed summation order (slice-strided, then the 8 slices in order).
+__global__ __launch_bounds__(256) void part_reduce_kernel(const float* __restrict__ part, int nb, long ld, int ncols,
+                                                          int seg, float* o0, float* o1, float* o2, int accumulate,
+                                                          const float* __restrict__ scale) {
+  __shared__ float red[8][33];
+  const int cx = threadIdx.x & 31, j = threadIdx.x >> 5;
+  const int c = blockIdx.x * 32 + cx;
+  float s0 = 0.f, s1 = 0.f;
+  if (c < ncols) {
+    int b = j;
+    for (; b + 8 < nb; b += 16) {
+      s0 += part[(long)b * ld + c];
+      s1 += part[(long)(b + 8) * ld + c];
+    }
+    if (b < nb) s0 += part[(long)b * ld + c];
+  }
+  red[j][cx] = s0 + s1;
+  __syncthreads();
+  if (j == 0 && c < ncols) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) t += red[i][cx];
+    if (scale) t *= *scale;
+    const int k = c / seg, col = c - k * seg;
+    float* o = k == 0 ? o0 : (k == 1 ? o1 : o2);
+    if (o) o[col] = accumulate ? o[col] + t : t;
+  }
+}
+void part_reduce(const float* part, int nb, long ld, int ncols, int seg, float* o0, float* o1, float* o2,
+                 int accumulate, const float* scale, hipStream_t st) {
+  hipLaunchKernelGGL(part_reduce_kernel, dim3(ceil_div(ncols, 32)), dim3(256), 0, st, part, nb, ld, ncols, seg, o0, o1,
+                     o2, accumulate, scale);
+}
+
 // ------------------------------------------------------------------ colsum
-// part[rb][n] = sum over the row chunk rb of x[m][n]
+// part[rb][n] = sum over row chunk rb of x[m][n]; block = 64 vec4 columns x 4 row phases.
 constexpr int CS_ROWBLK = 256;
 template <typename T>
 __global__ __launch_bounds__(256) void colsum_part_kernel(const T* __restrict__ x, long ldx, int M, int N,
                                                           float* __restrict__ part, int rows_per_blk) {
-  const int c4 = blockIdx.x * 256 + threadIdx.x;  // vec4 column index
-  if (c4 * 4 >= N) return;
+  __shared__ f32x4 red[4][64];
+  const int c4 = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int j = threadIdx.x >> 6;
   const int r0 = blockIdx.y * rows_per_blk, r1 = min(M, r0 + rows_per_blk);
-  f32x4 s = {0.f, 0.f, 0.f, 0.f};
-  for (int r = r0; r < r1; ++r) s += load4<T>(x + (long)r * ldx + c4 * 4);
-  *(f32x4*)(part + (long)blockIdx.y * N + c4 * 4) = s;
+  f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = s0;
+  if (c4 * 4 < N) {
+    int r = r0 + j;
+    for (; r + 4 < r1; r += 8) {
+      s0 += load4<T>(x + (long)r * ldx + c4 * 4);
+      s1 += load4<T>(x + (long)(r + 4) * ldx + c4 * 4);
+    }
+    if (r < r1) s0 += load4<T>(x + (long)r * ldx + c4 * 4);
+  }
+  red[j][threadIdx.x & 63] = s0 + s1;
+  __syncthreads();
+  if (j == 0 && c4 * 4 < N) {
+    const int t = threadIdx.x & 63;
+    *(f32x4*)(part + (long)blockIdx.y * N + c4 * 4) = red[0][t] + red[1][t] + red[2][t] + red[3][t];
+  }
 }
-__global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restrict__ part, int nblk, int N,
-                                                           float* out, int accumulate, const float* scale) {
-  const int n = blockIdx.x * 256 + threadIdx.x;
-  if (n >= N) return;
-  float s = 0.f;
-  for (int b = 0; b < nblk; ++b) s += part[(long)b * N + n];
-  if (scale) s *= *scale;
-  out[n] = accumulate ? out[n] + s : s;
-}
-static int colsum_nblk(int M) { return std::max(1, std::min(ceil_div(M, 64), CS_ROWBLK)); }
+static int colsum_nblk(int M) { return std::max(1, std::min(ceil_div(M, 128), CS_ROWBLK)); }
 
 // ------------------------------------------------------------------ im2col
 template <typename T>
@@ -587,13 +628,12 @@ extern "C" int fer_colsum(int dtype, const void* x, int64_t ldx, int M, int N, f
   if (!ws || ws_bytes < fer_colsum_ws(M, N)) return set_error("colsum: workspace too small");
   const int rpb = ceil_div(std::max(M, 1), nblk);
   hipStream_t st = (hipStream_t)stream;
-  dim3 grid(ceil_div(N / 4, 256), nblk);
+  dim3 grid(ceil_div(N / 4, 64), nblk);
   if (dtype == FER_BF16)
     hipLaunchKernelGGL(colsum_part_kernel<bf16>, grid, dim3(256), 0, st, (const bf16*)x, (long)ldx, M, N, ws, rpb);
   else
     hipLaunchKernelGGL(colsum_part_kernel<float>, grid, dim3(256), 0, st, (const float*)x, (long)ldx, M, N, ws, rpb);
-  hipLaunchKernelGGL(colsum_final_kernel, dim3(ceil_div(N, 256)), dim3(256), 0, st, ws, nblk, N, out, accumulate,
-                     scale_ptr);
+  part_reduce(ws, nblk, N, N, N, out, nullptr, nullptr, accumulate, scale_ptr, st);
   return hip_check("colsum");
 }
 
@@ -644,8 +684,8 @@ extern "C" int fer_tokens_bwd(int dtype, const void* dt, void* demb, float* dcls
   else
     hipLaunchKernelGGL(tokens_bwd_kernel<float>, grid, dim3(256), 0, st, (const float*)dt, (float*)demb, B, n, D,
                        drop_thresh, drop_scale, seed, ws, bchunk);
-  hipLaunchKernelGGL(tokens_bwd_final, dim3(ceil_div((long)N * D, 256)), dim3(256), 0, st, ws, nch, N, D, dcls, dpos,
-                     accumulate);
+  if (dpos) part_reduce(ws, nch, (long)N * D, N * D, N * D, dpos, nullptr, nullptr, accumulate, nullptr, st);
+  if (dcls) part_reduce(ws, nch, (long)N * D, D, D, dcls, nullptr, nullptr, accumulate, nullptr, st);
   return hip_check("tokens_bwd");
 }
 
@@ -691,8 +731,9 @@ extern "C" int fer_head_bwd(int dtype, const void* t, int64_t row_stride, const 
     hipLaunchKernelGGL(head_bwd_kernel<float>, dim3(B), dim3(256), 0, st, (const float*)t, (long)row_stride, ln_w,
                        ln_b, W, stats, dlogits, (float*)dt, D, C, drop_thresh, drop_scale, seed, ws);
   const long ps = (long)C * D + C + 2 * D;
-  hipLaunchKernelGGL(head_bwd_final, dim3(ceil_div(ps, 256)), dim3(256), 0, st, ws, B, C, D, dW, dbias, dln_w, dln_b,
-                     accumulate);
+  if (dW) part_reduce(ws, B, ps, C * D, C * D, dW, nullptr, nullptr, accumulate, nullptr, st);
+  if (dbias) part_reduce(ws + (long)C * D, B, ps, C, C, dbias, nullptr, nullptr, accumulate, nullptr, st);
+  if (dln_w || dln_b) part_reduce(ws + (long)C * D + C, B, ps, 2 * D, D, dln_w, dln_b, nullptr, accumulate, nullptr, st);
   return hip_check("head_bwd");
 }
 

@@ -62,9 +62,12 @@ WS = _Workspace()
 
 
 def drop_args(p: float):
+    """(thresh, scale): an element is dropped iff its 16-bit uniform < thresh = round(p*65536)."""
     if p <= 0.0:
         return 0, 1.0
-    thr = min(int(p * 4294967296.0), 4294967295)
+    if p >= 1.0:
+        return 65536, 0.0
+    thr = max(1, min(65535, int(round(p * 65536.0))))
     return thr, 1.0 / (1.0 - p)
 
 

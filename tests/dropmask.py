@@ -1,26 +1,36 @@
-"""Host replica of the kernels' counter-based dropout hash (csrc/common.h fer_hash),
-so tests can rebuild the exact keep-mask a kernel used."""
+"""Host replica of the kernels' counter-based dropout hash (csrc/common.h fer_hash /
+drop_keep), so tests can rebuild the exact keep-mask a kernel used."""
 import numpy as np
 import torch
 
-_G = np.uint64(0x9E3779B97F4A7C15)
-_M = np.uint64(0xD6E8FEB86659FD93)
+_M32 = np.uint64(0xFFFFFFFF)
 
 
-def fer_hash(seed: int, idx: np.ndarray) -> np.ndarray:
+def _u32(x):
+    return np.asarray(x, dtype=np.uint64) & _M32
+
+
+def fer_hash(seed: int, pair: np.ndarray) -> np.ndarray:
+    pair = pair.astype(np.uint64)
+    s_lo, s_hi = np.uint64(seed & 0xFFFFFFFF), np.uint64((seed >> 32) & 0xFFFFFFFF)
     with np.errstate(over="ignore"):
-        z = idx.astype(np.uint64) + np.uint64(seed & 0xFFFFFFFFFFFFFFFF) * _G
-        z ^= z >> np.uint64(32)
-        z *= _M
-        z ^= z >> np.uint64(32)
-        z *= _M
-        z ^= z >> np.uint64(32)
-    return (z & np.uint64(0xFFFFFFFF)).astype(np.uint64)
+        x = _u32(_u32(pair) * np.uint64(0x9E3779B1) + s_lo)
+        x = x ^ _u32(_u32(pair >> np.uint64(32)) * np.uint64(0x85EBCA6B) + s_hi)
+        x ^= x >> np.uint64(16)
+        x = _u32(x * np.uint64(0x7FEB352D))
+        x ^= x >> np.uint64(15)
+        x = _u32(x * np.uint64(0x846CA68B))
+        x ^= x >> np.uint64(16)
+    return x
+
+
+def thresh(p: float) -> int:
+    return max(1, min(65535, int(round(p * 65536.0))))
 
 
 def keep_mask(seed: int, shape, p: float, base: int = 0) -> torch.Tensor:
-    thr = min(int(p * 4294967296.0), 4294967295)
     n = int(np.prod(shape))
     idx = np.arange(base, base + n, dtype=np.uint64)
-    k = fer_hash(seed, idx) >= np.uint64(thr)
-    return torch.from_numpy(k.reshape(shape))
+    h = fer_hash(seed, idx >> np.uint64(1))
+    u = (h >> ((idx & np.uint64(1)) * np.uint64(16))) & np.uint64(0xFFFF)
+    return torch.from_numpy((u >= np.uint64(thresh(p))).reshape(shape))
