@@ -9,13 +9,12 @@
 //   dgrad    dX = dY W       : A=dY (KC), B=W (MN)
 //   wgrad    dW = dY^T X     : A=dY (MN), B=X (MN), K = rows = B*N tokens (split-K)
 //
-// bf16 path: v_mfma_f32_16x16x32_bf16 (fp32 accumulate), K-step BK = 32, a 4-deep ring of
-// LDS stages filled by LDS-DMA (buffer_load ... lds, 16 B/lane) three K-steps ahead of the
-// MFMAs; each wave waits with a COUNTED vmcnt (only the stage it is about to read) and the
-// stages are handed between waves by a raw s_barrier (no vmcnt(0) drain in the loop).
+// bf16 path: v_mfma_f32_16x16x32_bf16 (fp32 accumulate), 256x256x64 tiles on 4 waves (one
+// per SIMD, 128x128 accumulators each), double-buffered LDS stages filled by LDS-DMA
+// (buffer_load ... lds, 16 B/lane) one K-step ahead, fragment reads software-pipelined.
 // The swizzle is applied on the per-lane SOURCE address (the DMA image is lane-linear):
-//   KC image  [rows][32 k]  (64 B rows):   chunk' = chunk ^ G[(row>>2)&3], G = {0,2,3,1}
-//   MN image  [32 k][rows]  (2*R B rows):  chunk' = chunk ^ (rho(k)<<1),
+//   KC image  [rows][64 k]  (128 B rows):  chunk' = chunk ^ ((row>>1)&7)
+//   MN image  [64 k][rows]  (2*R B rows):  chunk' = chunk ^ (rho(k)<<1),
 //                                          rho(k) = (k&3) | ((k>>3)&1)<<2
 // KC fragments are read with ds_read_b128, MN fragments with two ds_read_b64_tr_b16
 // (hardware transpose); both images are bank-conflict free for their reads.
@@ -24,6 +23,8 @@
 // lane ends with 4 consecutive n of one m (8/16-byte epilogue accesses).
 //
 // fp32 path (parity mode): a plain LDS-tiled VALU kernel with the same epilogue.
+#include <stdlib.h>
+
 #include "common.h"
 #include "fervit_internal.h"
 
@@ -78,51 +79,87 @@ FER_DEV void tile_of(int bid, int tiles_m, int tiles_n, int& tm, int& tn) {
 }
 
 // ------------------------------------------------------------- LDS-DMA stage
-constexpr int BK = 32;
-FER_DEV int kc_swz(int row) { return (0x78 >> (2 * ((row >> 2) & 3))) & 3; }
-FER_DEV int mn_rho(int k) { return (k & 3) | (((k >> 3) & 1) << 2); }
+constexpr int BK = 64;
+FER_DEV int kc_swz(int row) { return (row >> 1) & 7; }
 
-template <int R, bool KC, int NW>
-FER_DEV void stage_tile(__amdgpu_buffer_rsrc_t rs, char* lds_tile, int wave, int lane, long ld, int r0,
-                        int rmax, int k0, int kmax) {
-  constexpr int NI = R * BK * 2 / 1024 / NW;  // 1 KiB wave-instructions per wave
+// Per-lane DMA source offsets of this wave's pieces, computed once per tile. For KC the
+// K-step adds k0*2 bytes; for MN it adds the wave-uniform k0*ld*2. `kof` is the lane's K
+// offset inside the stage, checked against the K tail only on the last K-step.
+template <int MT> FER_DEV int mn_swz_t(int k);
+
+template <int R, bool KC, int NW, int MT>
+struct DmaPlan {
+  static constexpr int NI = R * BK * 2 / 1024 / NW;
   static_assert(NI * NW * 1024 == R * BK * 2, "tile/wave mismatch");
+  uint32_t off[NI];
+  int kof[NI];
+  bool ok[NI];
+  FER_DEV void init(int wave, int lane, long ld, int r0, int rmax) {
 #pragma unroll
-  for (int i = 0; i < NI; ++i) {
-    const int gi = wave * NI + i;
-    uint32_t voff;
-    if constexpr (KC) {
-      const int row = gi * 16 + (lane >> 2);
-      const int c = (lane & 3) ^ kc_swz(row);
-      const int gr = r0 + row, gk = k0 + c * 8;
-      voff = (gr < rmax && gk < kmax) ? (uint32_t)(((long)gr * ld + gk) * 2) : FER_OOB;
-    } else {
-      constexpr int RB = R * 2;
-      const int byte = gi * 1024 + lane * 16;
-      const int k = byte / RB;
-      const int cp = (byte % RB) >> 4;
-      const int c = cp ^ (mn_rho(k) << 1);
-      const int gk = k0 + k, gc = r0 + c * 8;
-      voff = (gk < kmax && gc < rmax) ? (uint32_t)(((long)gk * ld + gc) * 2) : FER_OOB;
+    for (int i = 0; i < NI; ++i) {
+      const int gi = wave * NI + i;
+      if constexpr (KC) {
+        const int row = gi * 8 + (lane >> 3);
+        const int c = (lane & 7) ^ kc_swz(row);
+        const int gr = r0 + row;
+        ok[i] = gr < rmax;
+        kof[i] = c * 8;
+        off[i] = (uint32_t)(((long)gr * ld + c * 8) * 2);
+      } else {
+        constexpr int RB = R * 2;
+        const int byte = gi * 1024 + lane * 16;
+        const int k = byte / RB;
+        const int c = ((byte % RB) >> 4) ^ mn_swz_t<MT>(k);
+        const int gc = r0 + c * 8;
+        ok[i] = gc < rmax;
+        kof[i] = k;
+        off[i] = (uint32_t)(((long)k * ld + gc) * 2);
+      }
     }
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(lds_tile + gi * 1024), 16, voff, 0, 0, 0);
   }
+  FER_DEV void issue(__amdgpu_buffer_rsrc_t rs, char* lds_tile, int wave, long ld, int k0, int kmax, bool tail,
+                     int p0, int np) const {
+    const uint32_t kadd = KC ? (uint32_t)(k0 * 2) : (uint32_t)(k0 * ld * 2);
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      if (i < p0 || i >= p0 + np) continue;
+      const bool v = ok[i] && (!tail || k0 + kof[i] < kmax);
+      const uint32_t voff = v ? off[i] + kadd : FER_OOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(lds_tile + (wave * NI + i) * 1024), 16, voff, 0, 0,
+                                               0);
+    }
+  }
+};
+
+// MFMA operand fragments. MT = 32: v_mfma_f32_32x32x16_bf16, lane l holds index i0 + (l&31),
+// k = 16kk + 8(l>>5) + j. MT = 16: v_mfma_f32_16x16x32_bf16, lane l holds index i0 + (l&15),
+// k = 32kk + 8(l>>4) + j (j = 0..7). KC images are read with ds_read_b128, MN images with two
+// ds_read_b64_tr_b16 (rows k..k+3 and k+4..k+7 of 16 consecutive indices).
+template <int MT> FER_DEV int mn_swz_t(int k) {
+  if constexpr (MT == 32) return (k & 3) << 2;               // 4 rows x 64 B per 32-lane half
+  else return ((k & 3) | (((k >> 3) & 1) << 2)) << 1;       // 8 rows x 32 B per 32-lane half
 }
 
-// 16 rows/cols x 32 k fragment: lane l holds index (l&15), k = 8*(l>>4) + j.
-template <int R, bool KC>
-FER_DEV bf16x8 read_frag(const char* lds_tile, int i0, int lane) {
+template <int MT, int R, bool KC>
+FER_DEV bf16x8 read_frag(const char* lds_tile, int i0, int kk, int lane) {
   if constexpr (KC) {
-    const int row = i0 + (lane & 15);
-    const int c = (lane >> 4) ^ kc_swz(row);
-    return *(const bf16x8*)(lds_tile + row * 64 + c * 16);
+    const int row = i0 + (MT == 32 ? (lane & 31) : (lane & 15));
+    const int ch = MT == 32 ? 2 * kk + (lane >> 5) : 4 * kk + (lane >> 4);
+    return *(const bf16x8*)(lds_tile + row * 128 + ((ch ^ kc_swz(row)) << 4));
   } else {
     constexpr int RB = R * 2;
-    const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
-    const int k1 = 8 * g + q, k2 = k1 + 4;
-    const int c = (i0 >> 3) + (p >> 1);
-    const char* a1 = lds_tile + k1 * RB + ((c ^ (mn_rho(k1) << 1)) << 4) + (p & 1) * 8;
-    const char* a2 = lds_tile + k2 * RB + ((c ^ (mn_rho(k2) << 1)) << 4) + (p & 1) * 8;
+    const int gg = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+    int k1, c;
+    if constexpr (MT == 32) {
+      k1 = 16 * kk + 8 * (gg >> 1) + q;
+      c = ((i0 + 16 * (gg & 1)) >> 3) + (p >> 1);
+    } else {
+      k1 = 32 * kk + 8 * gg + q;
+      c = (i0 >> 3) + (p >> 1);
+    }
+    const int k2 = k1 + 4;
+    const char* a1 = lds_tile + k1 * RB + ((c ^ mn_swz_t<MT>(k1)) << 4) + (p & 1) * 8;
+    const char* a2 = lds_tile + k2 * RB + ((c ^ mn_swz_t<MT>(k2)) << 4) + (p & 1) * 8;
     short4_t t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4_t*)a1);
     short4_t t2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4_t*)a2);
     bf16x4 b1 = __builtin_bit_cast(bf16x4, t1), b2 = __builtin_bit_cast(bf16x4, t2);
@@ -135,16 +172,37 @@ FER_DEV void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int BM, int BN, int WM, int WN, bool AKC, bool BKC, int STAGES>
+template <int MT> struct Acc;
+template <> struct Acc<32> { typedef f32x16 T; };
+template <> struct Acc<16> { typedef f32x4 T; };
+
+template <int MT>
+FER_DEV typename Acc<MT>::T mfma(bf16x8 a, bf16x8 b, typename Acc<MT>::T c) {
+  if constexpr (MT == 32) return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+  else return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// Wave grid WM x WN over a BM x BN tile; each wave owns (BM/WM) x (BN/WN) as MT x MT MFMA
+// blocks. The MFMA is issued with the B fragment as the instruction's A operand, so the
+// accumulator's column index is m: for MT=32, lane l holds m = l&31 and n = 8q + 4(l>>5) + r
+// (q, r = 0..3); for MT=16, m = l&15 and n = 4(l>>4) + r.
+// Double-buffered BK=64 stages. Per K-step t the SS substeps run  ds_read(t, kk+1) | 1/SS of
+// the DMA pieces of stage t+1 | MFMAs(t, kk), then vmcnt(0) + s_barrier hands stage t+1 over.
+template <int BM, int BN, int WM, int WN, bool AKC, bool BKC, int MT>
 __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g, EpiArgs e) {
+  typedef typename Acc<MT>::T AccT;
   constexpr int NW = WM * WN;
   constexpr int TM = BM / WM, TN = BN / WN;
-  constexpr int FM = TM / 16, FN = TN / 16;
+  constexpr int FM = TM / MT, FN = TN / MT;
+  constexpr int SS = MT == 32 ? 4 : 2;
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
   constexpr int STAGE = A_BYTES + B_BYTES;
-  constexpr int LPW = STAGE / 1024 / NW;  // LDS-DMA instructions per wave per stage
-  static_assert(STAGES == 4, "vmcnt ladder below assumes a 4-deep ring");
-  __shared__ __attribute__((aligned(1024))) char smem[STAGES * STAGE];
+  constexpr int NA = A_BYTES / 1024 / NW, NB = B_BYTES / 1024 / NW;  // DMA pieces per wave
+  constexpr int QA = (NA + SS - 1) / SS, QB = (NB + SS - 1) / SS;     // per substep
+  constexpr int EROWS = BM / 2, ELD = BN + 4;                         // epilogue staging: half tile fp32
+  constexpr int SMEM = (2 * STAGE > EROWS * ELD * 4) ? 2 * STAGE : EROWS * ELD * 4;
+  static_assert(WM == 2, "epilogue staging splits the tile by the wave-row halves");
+  __shared__ __attribute__((aligned(1024))) char smem[SMEM];
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -160,70 +218,118 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g, 
 
   const __amdgpu_buffer_rsrc_t ra = make_rsrc(g.A);
   const __amdgpu_buffer_rsrc_t rb = make_rsrc(g.B);
+  DmaPlan<BM, AKC, NW, MT> pa;
+  DmaPlan<BN, BKC, NW, MT> pb;
+  pa.init(wave, lane, g.lda, m0, g.M);
+  pb.init(wave, lane, g.ldb, n0, g.N);
+  const int ktail = kbeg + (nk - 1) * BK;  // first K of the last step (only step that can be partial)
 
-  f32x4 acc[FN][FM];
+  AccT acc[FN][FM];
 #pragma unroll
   for (int i = 0; i < FN; ++i)
 #pragma unroll
-    for (int j = 0; j < FM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < FM; ++j) acc[i][j] = AccT{};
 
-  // prologue: K-steps 0..STAGES-2 in flight
-#pragma unroll
-  for (int s = 0; s < STAGES - 1; ++s) {
-    if (s < nk) {
-      char* dst = smem + s * STAGE;
-      stage_tile<BM, AKC, NW>(ra, dst, wave, lane, g.lda, m0, g.M, kbeg + s * BK, kend);
-      stage_tile<BN, BKC, NW>(rb, dst + A_BYTES, wave, lane, g.ldb, n0, g.N, kbeg + s * BK, kend);
-    }
-  }
-  for (int t = 0; t < nk; ++t) {
-    // this wave's DMA for K-step t has landed: leave the younger stages in flight
-    const int younger = min(STAGES - 2, nk - 1 - t);
-    if (younger >= 2) wait_vm<2 * LPW>();
-    else if (younger == 1) wait_vm<LPW>();
-    else wait_vm<0>();
-    // every wave's DMA for t landed, and every wave is done reading stage (t-1)
+  bf16x8 af[FM], bfr[FN];
+  if (nk > 0) {
+    pa.issue(ra, smem, wave, g.lda, kbeg, kend, kbeg == ktail, 0, NA);
+    pb.issue(rb, smem + A_BYTES, wave, g.ldb, kbeg, kend, kbeg == ktail, 0, NB);
+    wait_vm<0>();
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (t + STAGES - 1 < nk) {
-      char* dst = smem + ((t + STAGES - 1) % STAGES) * STAGE;
-      const int k0 = kbeg + (t + STAGES - 1) * BK;
-      stage_tile<BM, AKC, NW>(ra, dst, wave, lane, g.lda, m0, g.M, k0, kend);
-      stage_tile<BN, BKC, NW>(rb, dst + A_BYTES, wave, lane, g.ldb, n0, g.N, k0, kend);
+#pragma unroll
+    for (int i = 0; i < FN; ++i) bfr[i] = read_frag<MT, BN, BKC>(smem + A_BYTES, wn * TN + i * MT, 0, lane);
+#pragma unroll
+    for (int j = 0; j < FM; ++j) af[j] = read_frag<MT, BM, AKC>(smem, wm * TM + j * MT, 0, lane);
+  }
+  for (int t = 0; t < nk; ++t) {
+    const char* cur = smem + (t & 1) * STAGE;
+    char* nxt = smem + ((t + 1) & 1) * STAGE;
+    const bool more = t + 1 < nk;
+    const int k1 = kbeg + (t + 1) * BK;
+#pragma unroll
+    for (int kk = 0; kk < SS; ++kk) {
+      bf16x8 an[FM], bn[FN];
+      if (kk < SS - 1) {
+#pragma unroll
+        for (int i = 0; i < FN; ++i) bn[i] = read_frag<MT, BN, BKC>(cur + A_BYTES, wn * TN + i * MT, kk + 1, lane);
+#pragma unroll
+        for (int j = 0; j < FM; ++j) an[j] = read_frag<MT, BM, AKC>(cur, wm * TM + j * MT, kk + 1, lane);
+      }
+      if (more) {
+        pa.issue(ra, nxt, wave, g.lda, k1, kend, k1 == ktail, kk * QA, QA);
+        pb.issue(rb, nxt + A_BYTES, wave, g.ldb, k1, kend, k1 == ktail, kk * QB, QB);
+      }
+#pragma unroll
+      for (int j = 0; j < FM; ++j)
+#pragma unroll
+        for (int i = 0; i < FN; ++i) acc[i][j] = mfma<MT>(bfr[i], af[j], acc[i][j]);
+      if (kk < SS - 1) {
+#pragma unroll
+        for (int i = 0; i < FN; ++i) bfr[i] = bn[i];
+#pragma unroll
+        for (int j = 0; j < FM; ++j) af[j] = an[j];
+      }
     }
-    const char* cur = smem + (t % STAGES) * STAGE;
-    bf16x8 af[FM], bfr[FN];
+    if (more) {
+      wait_vm<0>();
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
 #pragma unroll
-    for (int i = 0; i < FN; ++i) bfr[i] = read_frag<BN, BKC>(cur + A_BYTES, wn * TN + i * 16, lane);
+      for (int i = 0; i < FN; ++i) bfr[i] = read_frag<MT, BN, BKC>(nxt + A_BYTES, wn * TN + i * MT, 0, lane);
 #pragma unroll
-    for (int j = 0; j < FM; ++j) af[j] = read_frag<BM, AKC>(cur, wm * TM + j * 16, lane);
-#pragma unroll
-    for (int j = 0; j < FM; ++j)
-#pragma unroll
-      for (int i = 0; i < FN; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[i], af[j], acc[i][j], 0, 0, 0);
+      for (int j = 0; j < FM; ++j) af[j] = read_frag<MT, BM, AKC>(nxt, wm * TM + j * MT, 0, lane);
+    }
   }
 
-  // ---- epilogue: lane holds C[m][n..n+3]
-  const long mb = m0 + wm * TM + (lane & 15);
-  const long nb = n0 + wn * TN + 4 * (lane >> 4);
+  // ---- epilogue. Accumulator element (i, j, q, r) -> tile row/col:
+  constexpr int NQ = MT == 32 ? 4 : 1;
+  const int lr = MT == 32 ? (lane & 31) : (lane & 15);
+  const int lc = MT == 32 ? 4 * (lane >> 5) : 4 * (lane >> 4);
   if (g.partial) {  // split-K partial slab, fp32 [split][M][N]
     float* ws = g.ws + (long)ks * g.M * g.N;
 #pragma unroll
     for (int i = 0; i < FN; ++i)
 #pragma unroll
-      for (int j = 0; j < FM; ++j) {
-        const long m = mb + j * 16, n = nb + i * 16;
-        if (m < g.M && n < g.N) *(f32x4*)(ws + m * g.N + n) = acc[i][j];
-      }
+      for (int j = 0; j < FM; ++j)
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+          const long m = m0 + wm * TM + j * MT + lr, n = n0 + wn * TN + i * MT + 8 * q + lc;
+          if (m < g.M && n < g.N)
+            *(f32x4*)(ws + m * g.N + n) =
+                f32x4{acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]};
+        }
     return;
   }
+  // Stage each half of the tile (the rows of wave-row wm == h) through LDS as fp32 with padded
+  // rows, then every thread applies the epilogue on 4 consecutive columns of one row: all
+  // global traffic of the epilogue (bias, pre, residual, aux, output) is row-contiguous.
+  float* ep = (float*)smem;
+  constexpr int NT = 64 * NW;
+  constexpr int C4 = BN / 4;  // float4 groups per row
 #pragma unroll
-  for (int i = 0; i < FN; ++i)
+  for (int h = 0; h < 2; ++h) {
+    __syncthreads();
+    if (wm == h) {
 #pragma unroll
-    for (int j = 0; j < FM; ++j) {
-      const long m = mb + j * 16, n = nb + i * 16;
-      if (m < g.M && n < g.N) epi4<bf16>(e, m, n, acc[i][j]);
+      for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int j = 0; j < FM; ++j)
+#pragma unroll
+          for (int q = 0; q < NQ; ++q) {
+            const int r = j * MT + lr;
+            const int c = wn * TN + i * MT + 8 * q + lc;
+            *(f32x4*)(ep + r * ELD + c) =
+                f32x4{acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]};
+          }
     }
+    __syncthreads();
+    for (int idx = threadIdx.x; idx < EROWS * C4; idx += NT) {
+      const int r = idx / C4, c = (idx - r * C4) * 4;
+      const long m = m0 + h * EROWS + r, n = n0 + c;
+      if (m < g.M && n < g.N) epi4<bf16>(e, m, n, *(const f32x4*)(ep + r * ELD + c));
+    }
+  }
 }
 
 // Ordered (deterministic) split-K reduction + epilogue.
@@ -283,20 +389,36 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs g, EpiArgs e, in
 }
 
 // -------------------------------------------------------------------- launch
-template <int BM, int BN, int WM, int WN, bool AKC, bool BKC>
+template <int BM, int BN, int WM, int WN, bool AKC, bool BKC, int MT>
 static int launch_bf16(GemmArgs g, const EpiArgs& e, hipStream_t st) {
   g.tiles_m = (g.M + BM - 1) / BM;
   g.tiles_n = (g.N + BN - 1) / BN;
   dim3 grid(g.tiles_m * g.tiles_n, g.splits);
-  hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, WM, WN, AKC, BKC, 4>), grid, dim3(64 * WM * WN), 0, st, g, e);
+  hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, WM, WN, AKC, BKC, MT>), grid, dim3(64 * WM * WN), 0, st, g, e);
   return 0;
+}
+
+static int forced_cfg() {
+  static int v = -2;
+  if (v == -2) {
+    const char* s = getenv("FERVIT_GEMM_CFG");
+    v = s ? atoi(s) : -1;
+  }
+  return v;
 }
 
 template <bool AKC, bool BKC>
 static int dispatch_tile(GemmArgs g, const EpiArgs& e, hipStream_t st) {
+  switch (forced_cfg()) {
+    case 0: return launch_bf16<256, 256, 2, 4, AKC, BKC, 32>(g, e, st);
+    case 1: return launch_bf16<256, 256, 2, 4, AKC, BKC, 16>(g, e, st);
+    case 2: return launch_bf16<128, 128, 2, 2, AKC, BKC, 32>(g, e, st);
+    case 3: return launch_bf16<128, 128, 2, 2, AKC, BKC, 16>(g, e, st);
+    default: break;
+  }
   const long t256 = ((g.M + 255) / 256) * ((g.N + 255) / 256) * (long)g.splits;
-  if (t256 >= 200) return launch_bf16<256, 256, 2, 4, AKC, BKC>(g, e, st);
-  return launch_bf16<128, 128, 2, 2, AKC, BKC>(g, e, st);
+  if (t256 >= 200) return launch_bf16<256, 256, 2, 4, AKC, BKC, 32>(g, e, st);
+  return launch_bf16<128, 128, 2, 2, AKC, BKC, 16>(g, e, st);
 }
 
 int gemm_launch(const GemmDesc& d, const EpiArgs& e_in, hipStream_t st) {

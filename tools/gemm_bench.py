@@ -1,0 +1,68 @@
+"""GEMM microbenchmark on the ViT-B/16 bs=256 shapes: libfervit bf16 GEMM (plain and
+with the real epilogues) vs torch.matmul (hipBLASLt) as a known-good reference.
+Interleaved rounds in one process (cdna guide §5.4 rule 24); random N(0,1) data."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "fer-vit_amd"))
+import torch  # noqa: E402
+
+from fervit import ops  # noqa: E402
+
+PEAK = 2516.6
+
+
+def timeit(fn, reps=20):
+    s = torch.cuda.current_stream()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    a.record(s)
+    for _ in range(reps):
+        fn()
+    b.record(s)
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / reps
+
+
+def main():
+    dev = "cuda"
+    M, D, F = 256 * 197, 768, 3072
+    g = torch.Generator(device=dev).manual_seed(0)
+    r = lambda *s: torch.randn(*s, device=dev, generator=g, dtype=torch.bfloat16)
+    x, w1, w2, wqkv = r(M, D), r(F, D) * 0.03, r(D, F) * 0.03, r(3 * D, D) * 0.03
+    h, dF = r(M, F), r(M, F)
+    b1 = torch.zeros(F, device=dev)
+    pre = torch.empty(M, F, device=dev, dtype=torch.bfloat16)
+    gw = torch.empty(F, D, device=dev)
+    cases = {
+        "fc1 fwd plain": (lambda: ops.linear_fwd(x, w1), 2 * M * F * D, lambda: x @ w1.t()),
+        "fc1 fwd +bias+gelu+drop+pre": (lambda: ops.linear_fwd(x, w1, b1, pre=pre, act="gelu", dropout=0.1, seed=7),
+                                         2 * M * F * D, None),
+        "fc2 fwd plain (K=3072)": (lambda: ops.linear_fwd(h, w2), 2 * M * F * D, lambda: h @ w2.t()),
+        "qkv fwd plain": (lambda: ops.linear_fwd(x, wqkv), 2 * M * 3 * D * D, lambda: x @ wqkv.t()),
+        "fc2 dgrad (B MN)": (lambda: ops.linear_dgrad(x, w2), 2 * M * F * D, lambda: x @ w2),
+        "fc1 wgrad (MN,MN splitK)": (lambda: ops.linear_wgrad(dF, x, gw), 2 * M * F * D, lambda: dF.t() @ x),
+    }
+    only = os.environ.get("GB_ONLY")
+    if only:
+        cases = {k: v for k, v in cases.items() if only in k}
+    res = {k: [] for k in cases}
+    ref = {k: [] for k in cases}
+    for _ in range(3):
+        for k, (fn, fl, tf) in cases.items():
+            res[k].append(timeit(fn))
+            if tf is not None:
+                ref[k].append(timeit(tf))
+    tag = os.environ.get("FERVIT_GEMM_CFG", "auto")
+    for k, (fn, fl, tf) in cases.items():
+        t = min(res[k])
+        line = f"[cfg {tag}] {k:32s} ours {t * 1e3:8.1f} us  {fl / t / 1e9:7.1f} TF ({fl / t / 1e9 / PEAK * 100:4.1f}%)"
+        if ref[k]:
+            tr = min(ref[k])
+            line += f"   hipBLASLt {tr * 1e3:8.1f} us {fl / tr / 1e9:7.1f} TF"
+        print(line, flush=True)
+
+
+if __name__ == "__main__":
+    main()
