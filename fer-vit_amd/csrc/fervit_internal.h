@@ -19,6 +19,7 @@ struct GemmArgs {
   int tiles_m, tiles_n;
   int splits, k_chunk, partial;
   float* ws;
+  int dbg;  // experiment switches (FERVIT_GEMM_DBG), 0 in production
 };
 
 int set_error(const char* msg);

@@ -41,6 +41,7 @@ FER_DEV void epi4(const EpiArgs& e, long m, long n, f32x4 v) {
     for (int r = 0; r < 4; ++r) v[r] = act_fwd(e.act, v[r]);
   }
   if (e.drop_thresh) drop4(e.seed, (uint64_t)m * (uint64_t)e.drop_ld + (uint64_t)n, e.drop_thresh, e.drop_scale, v);
+  if (e.post_scale) v *= *e.post_scale;
   if (e.aux) {
     f32x4 a = load4<T>((const T*)e.aux + m * e.ldx + n);
 #pragma unroll
@@ -82,49 +83,54 @@ FER_DEV void tile_of(int bid, int tiles_m, int tiles_n, int& tm, int& tn) {
 constexpr int BK = 64;
 FER_DEV int kc_swz(int row) { return (row >> 1) & 7; }
 
-// Per-lane DMA source offsets of this wave's pieces, computed once per tile. For KC the
-// K-step adds k0*2 bytes; for MN it adds the wave-uniform k0*ld*2. `kof` is the lane's K
-// offset inside the stage, checked against the K tail only on the last K-step.
-template <int MT> FER_DEV int mn_swz_t(int k);
+// Per-lane DMA source offsets of this wave's pieces, computed once per tile; an
+// out-of-range row/column gets base FER_OOB so voffset = base + k-advance stays out of range
+// (one add per piece per K-step). For KC the K-step adds k0*2 bytes, for MN the wave-uniform
+// k0*ld*2. `kof` (the lane's K inside the stage) is checked only on a partial last K-step.
+// MN tr-read image swizzle (16-byte chunk XOR by K row), see read_frag.
+template <int MT> FER_DEV int mn_swz_t(int k) {
+  if constexpr (MT == 32) return (k & 3) << 2;               // 4 rows x 64 B per 32-lane half
+  else return ((k & 3) | (((k >> 3) & 1) << 2)) << 1;       // 8 rows x 32 B per 32-lane half
+}
 
 template <int R, bool KC, int NW, int MT>
 struct DmaPlan {
   static constexpr int NI = R * BK * 2 / 1024 / NW;
   static_assert(NI * NW * 1024 == R * BK * 2, "tile/wave mismatch");
-  uint32_t off[NI];
+  uint32_t base[NI];
   int kof[NI];
-  bool ok[NI];
   FER_DEV void init(int wave, int lane, long ld, int r0, int rmax) {
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
       const int gi = wave * NI + i;
+      bool ok;
+      uint32_t off;
       if constexpr (KC) {
         const int row = gi * 8 + (lane >> 3);
         const int c = (lane & 7) ^ kc_swz(row);
         const int gr = r0 + row;
-        ok[i] = gr < rmax;
+        ok = gr < rmax;
         kof[i] = c * 8;
-        off[i] = (uint32_t)(((long)gr * ld + c * 8) * 2);
+        off = (uint32_t)(((long)gr * ld + c * 8) * 2);
       } else {
         constexpr int RB = R * 2;
         const int byte = gi * 1024 + lane * 16;
         const int k = byte / RB;
         const int c = ((byte % RB) >> 4) ^ mn_swz_t<MT>(k);
         const int gc = r0 + c * 8;
-        ok[i] = gc < rmax;
+        ok = gc < rmax;
         kof[i] = k;
-        off[i] = (uint32_t)(((long)k * ld + gc) * 2);
+        off = (uint32_t)(((long)k * ld + gc) * 2);
       }
+      base[i] = ok ? off : FER_OOB;
     }
   }
-  FER_DEV void issue(__amdgpu_buffer_rsrc_t rs, char* lds_tile, int wave, long ld, int k0, int kmax, bool tail,
-                     int p0, int np) const {
+  FER_DEV void issue(__amdgpu_buffer_rsrc_t rs, char* lds_tile, int wave, long ld, int k0, int kmax,
+                     bool tail) const {
     const uint32_t kadd = KC ? (uint32_t)(k0 * 2) : (uint32_t)(k0 * ld * 2);
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
-      if (i < p0 || i >= p0 + np) continue;
-      const bool v = ok[i] && (!tail || k0 + kof[i] < kmax);
-      const uint32_t voff = v ? off[i] + kadd : FER_OOB;
+      const uint32_t voff = (!tail || k0 + kof[i] < kmax) ? base[i] + kadd : FER_OOB;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(lds_tile + (wave * NI + i) * 1024), 16, voff, 0, 0,
                                                0);
     }
@@ -135,10 +141,6 @@ struct DmaPlan {
 // k = 16kk + 8(l>>5) + j. MT = 16: v_mfma_f32_16x16x32_bf16, lane l holds index i0 + (l&15),
 // k = 32kk + 8(l>>4) + j (j = 0..7). KC images are read with ds_read_b128, MN images with two
 // ds_read_b64_tr_b16 (rows k..k+3 and k+4..k+7 of 16 consecutive indices).
-template <int MT> FER_DEV int mn_swz_t(int k) {
-  if constexpr (MT == 32) return (k & 3) << 2;               // 4 rows x 64 B per 32-lane half
-  else return ((k & 3) | (((k >> 3) & 1) << 2)) << 1;       // 8 rows x 32 B per 32-lane half
-}
 
 template <int MT, int R, bool KC>
 FER_DEV bf16x8 read_frag(const char* lds_tile, int i0, int kk, int lane) {
@@ -186,8 +188,8 @@ FER_DEV typename Acc<MT>::T mfma(bf16x8 a, bf16x8 b, typename Acc<MT>::T c) {
 // blocks. The MFMA is issued with the B fragment as the instruction's A operand, so the
 // accumulator's column index is m: for MT=32, lane l holds m = l&31 and n = 8q + 4(l>>5) + r
 // (q, r = 0..3); for MT=16, m = l&15 and n = 4(l>>4) + r.
-// Double-buffered BK=64 stages. Per K-step t the SS substeps run  ds_read(t, kk+1) | 1/SS of
-// the DMA pieces of stage t+1 | MFMAs(t, kk), then vmcnt(0) + s_barrier hands stage t+1 over.
+// Double-buffered BK=64 stages. Per K-step t: all LDS-DMA pieces of stage t+1, then SS
+// substeps of  ds_read(t, kk+1) | MFMAs(t, kk); then vmcnt(0) + s_barrier hands t+1 over.
 template <int BM, int BN, int WM, int WN, bool AKC, bool BKC, int MT>
 __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g, EpiArgs e) {
   typedef typename Acc<MT>::T AccT;
@@ -197,8 +199,6 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g, 
   constexpr int SS = MT == 32 ? 4 : 2;
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
   constexpr int STAGE = A_BYTES + B_BYTES;
-  constexpr int NA = A_BYTES / 1024 / NW, NB = B_BYTES / 1024 / NW;  // DMA pieces per wave
-  constexpr int QA = (NA + SS - 1) / SS, QB = (NB + SS - 1) / SS;     // per substep
   constexpr int EROWS = BM / 2, ELD = BN + 4;                         // epilogue staging: half tile fp32
   constexpr int SMEM = (2 * STAGE > EROWS * ELD * 4) ? 2 * STAGE : EROWS * ELD * 4;
   static_assert(WM == 2, "epilogue staging splits the tile by the wave-row halves");
@@ -232,8 +232,8 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g, 
 
   bf16x8 af[FM], bfr[FN];
   if (nk > 0) {
-    pa.issue(ra, smem, wave, g.lda, kbeg, kend, kbeg == ktail, 0, NA);
-    pb.issue(rb, smem + A_BYTES, wave, g.ldb, kbeg, kend, kbeg == ktail, 0, NB);
+    pa.issue(ra, smem, wave, g.lda, kbeg, kend, kbeg == ktail);
+    pb.issue(rb, smem + A_BYTES, wave, g.ldb, kbeg, kend, kbeg == ktail);
     wait_vm<0>();
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
@@ -247,31 +247,32 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g, 
     char* nxt = smem + ((t + 1) & 1) * STAGE;
     const bool more = t + 1 < nk;
     const int k1 = kbeg + (t + 1) * BK;
+    // the whole of stage t+1 goes out first: it has the full K-step to land
+    if (more && !(g.dbg & 1)) {
+      pa.issue(ra, nxt, wave, g.lda, k1, kend, k1 == ktail);
+      pb.issue(rb, nxt + A_BYTES, wave, g.ldb, k1, kend, k1 == ktail);
+    }
 #pragma unroll
     for (int kk = 0; kk < SS; ++kk) {
       bf16x8 an[FM], bn[FN];
-      if (kk < SS - 1) {
+      if (kk < SS - 1 && !(g.dbg & 8)) {
 #pragma unroll
         for (int i = 0; i < FN; ++i) bn[i] = read_frag<MT, BN, BKC>(cur + A_BYTES, wn * TN + i * MT, kk + 1, lane);
 #pragma unroll
         for (int j = 0; j < FM; ++j) an[j] = read_frag<MT, BM, AKC>(cur, wm * TM + j * MT, kk + 1, lane);
       }
-      if (more) {
-        pa.issue(ra, nxt, wave, g.lda, k1, kend, k1 == ktail, kk * QA, QA);
-        pb.issue(rb, nxt + A_BYTES, wave, g.ldb, k1, kend, k1 == ktail, kk * QB, QB);
-      }
 #pragma unroll
       for (int j = 0; j < FM; ++j)
 #pragma unroll
         for (int i = 0; i < FN; ++i) acc[i][j] = mfma<MT>(bfr[i], af[j], acc[i][j]);
-      if (kk < SS - 1) {
+      if (kk < SS - 1 && !(g.dbg & 8)) {
 #pragma unroll
         for (int i = 0; i < FN; ++i) bfr[i] = bn[i];
 #pragma unroll
         for (int j = 0; j < FM; ++j) af[j] = an[j];
       }
     }
-    if (more) {
+    if (more && !(g.dbg & 2)) {
       wait_vm<0>();
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
@@ -282,6 +283,10 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g, 
     }
   }
 
+  if (g.dbg & 4) {
+    if (acc[0][0][0] == 12345.f) g.ws[0] = 1.f;  // keep the MFMAs alive
+    return;
+  }
   // ---- epilogue. Accumulator element (i, j, q, r) -> tile row/col:
   constexpr int NQ = MT == 32 ? 4 : 1;
   const int lr = MT == 32 ? (lane & 31) : (lane & 15);
@@ -416,8 +421,11 @@ static int dispatch_tile(GemmArgs g, const EpiArgs& e, hipStream_t st) {
     case 3: return launch_bf16<128, 128, 2, 2, AKC, BKC, 16>(g, e, st);
     default: break;
   }
+  // measured on MI355X (tools/gemm_bench.py): 256^2 / 8 waves / 32x32x16 for the forward and
+  // dgrad layouts when the grid fills the chip; 128^2 / 4 waves / 16x16x32 (2 blocks per CU)
+  // for split-K weight gradients and small problems.
   const long t256 = ((g.M + 255) / 256) * ((g.N + 255) / 256) * (long)g.splits;
-  if (t256 >= 200) return launch_bf16<256, 256, 2, 4, AKC, BKC, 32>(g, e, st);
+  if (AKC && t256 >= 200) return launch_bf16<256, 256, 2, 4, AKC, BKC, 32>(g, e, st);
   return launch_bf16<128, 128, 2, 2, AKC, BKC, 16>(g, e, st);
 }
 
@@ -426,6 +434,8 @@ int gemm_launch(const GemmDesc& d, const EpiArgs& e_in, hipStream_t st) {
   GemmArgs g{};
   g.A = d.A; g.B = d.B; g.lda = d.lda; g.ldb = d.ldb;
   g.M = d.M; g.N = d.N; g.K = d.K;
+  static const int dbg = getenv("FERVIT_GEMM_DBG") ? atoi(getenv("FERVIT_GEMM_DBG")) : 0;
+  g.dbg = dbg;
   if (d.M <= 0 || d.N <= 0) return 0;
   if (d.N % 4) return set_error("gemm: N must be a multiple of 4");
   if (d.dtype == FER_F32) {

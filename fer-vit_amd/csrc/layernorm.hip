@@ -65,7 +65,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, l
                                                      T* __restrict__ dx, long lddx, T* __restrict__ dxd,
                                                      uint32_t thr, float dscale, uint64_t seed,
                                                      float* __restrict__ part, int want_part, int M, int D) {
-  __shared__ float red[4][3][LN_VPL * 256];
+  __shared__ float red[4][LN_VPL * 256];  // one partial at a time: 16 KB keeps 4+ blocks/CU
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int nv = D >> 2;
   f32x4 pg[LN_VPL], pb[LN_VPL], pd[LN_VPL];
@@ -111,16 +111,13 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, l
   }
   if (!want_part) return;
 #pragma unroll
-  for (int i = 0; i < LN_VPL; ++i) {
-    const int c = lane + i * 64;
-    *(f32x4*)&red[w][0][c * 4] = pg[i];
-    *(f32x4*)&red[w][1][c * 4] = pb[i];
-    *(f32x4*)&red[w][2][c * 4] = pd[i];
-  }
-  __syncthreads();
-  for (int c = threadIdx.x; c < 3 * D; c += 256) {
-    const int k = c / D, col = c - k * D;
-    part[(long)blockIdx.x * 3 * D + c] = red[0][k][col] + red[1][k][col] + red[2][k][col] + red[3][k][col];
+  for (int k = 0; k < 3; ++k) {
+    if (k) __syncthreads();
+#pragma unroll
+    for (int i = 0; i < LN_VPL; ++i) *(f32x4*)&red[w][(lane + i * 64) * 4] = k == 0 ? pg[i] : (k == 1 ? pb[i] : pd[i]);
+    __syncthreads();
+    for (int c = threadIdx.x; c < D; c += 256)
+      part[((long)blockIdx.x * 3 + k) * D + c] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
   }
 }
 
@@ -137,7 +134,7 @@ __global__ __launch_bounds__(256) void ln_part_reduce_kernel(const float* __rest
   o[col] = accumulate ? o[col] + s : s;
 }
 
-static int ln_bwd_blocks(int M) { return std::max(1, std::min(ceil_div(M, 4), 256)); }
+static int ln_bwd_blocks(int M) { return std::max(1, std::min(ceil_div(M, 16), 1024)); }
 
 }  // namespace fer
 
