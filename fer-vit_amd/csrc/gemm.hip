@@ -81,7 +81,13 @@ FER_DEV void tile_of(int bid, int tiles_m, int tiles_n, int& tm, int& tn) {
 
 // ------------------------------------------------------------- LDS-DMA stage
 constexpr int BK = 64;
-FER_DEV int kc_swz(int row) { return (row >> 1) & 7; }
+// KC image [rows][BKT k] (2*BKT-byte rows). BKT=64: chunk ^= (row>>1)&7. BKT=32 (4 rows per
+// 256 B): chunk ^= s(row>>2) with s = 0,0,2,2,1,1,3,3 — conflict-free for the ds_read_b128
+// lane groups of both the 32x32 (16 rows, one chunk) and 16x16 (rows x 2 chunks) reads.
+template <int BKT> FER_DEV int kc_swz(int row) {
+  if constexpr (BKT == 64) return (row >> 1) & 7;
+  else return (((row >> 3) & 1) << 1) | ((row >> 4) & 1);
+}
 
 // Per-lane DMA source offsets of this wave's pieces, computed once per tile; an
 // out-of-range row/column gets base FER_OOB so voffset = base + k-advance stays out of range
@@ -93,10 +99,10 @@ template <int MT> FER_DEV int mn_swz_t(int k) {
   else return ((k & 3) | (((k >> 3) & 1) << 2)) << 1;       // 8 rows x 32 B per 32-lane half
 }
 
-template <int R, bool KC, int NW, int MT>
+template <int R, bool KC, int NW, int MT, int BKT = BK>
 struct DmaPlan {
-  static constexpr int NI = R * BK * 2 / 1024 / NW;
-  static_assert(NI * NW * 1024 == R * BK * 2, "tile/wave mismatch");
+  static constexpr int NI = R * BKT * 2 / 1024 / NW;
+  static_assert(NI * NW * 1024 == R * BKT * 2, "tile/wave mismatch");
   uint32_t base[NI];
   int kof[NI];
   FER_DEV void init(int wave, int lane, long ld, int r0, int rmax) {
@@ -106,8 +112,9 @@ struct DmaPlan {
       bool ok;
       uint32_t off;
       if constexpr (KC) {
-        const int row = gi * 8 + (lane >> 3);
-        const int c = (lane & 7) ^ kc_swz(row);
+        constexpr int CPR = BKT / 8;  // 16-byte chunks per row
+        const int row = gi * (64 / CPR) + lane / CPR;
+        const int c = (lane % CPR) ^ kc_swz<BKT>(row);
         const int gr = r0 + row;
         ok = gr < rmax;
         kof[i] = c * 8;
@@ -142,12 +149,12 @@ struct DmaPlan {
 // k = 32kk + 8(l>>4) + j (j = 0..7). KC images are read with ds_read_b128, MN images with two
 // ds_read_b64_tr_b16 (rows k..k+3 and k+4..k+7 of 16 consecutive indices).
 
-template <int MT, int R, bool KC>
+template <int MT, int R, bool KC, int BKT = BK>
 FER_DEV bf16x8 read_frag(const char* lds_tile, int i0, int kk, int lane) {
   if constexpr (KC) {
     const int row = i0 + (MT == 32 ? (lane & 31) : (lane & 15));
     const int ch = MT == 32 ? 2 * kk + (lane >> 5) : 4 * kk + (lane >> 4);
-    return *(const bf16x8*)(lds_tile + row * 128 + ((ch ^ kc_swz(row)) << 4));
+    return *(const bf16x8*)(lds_tile + row * (BKT * 2) + ((ch ^ kc_swz<BKT>(row)) << 4));
   } else {
     constexpr int RB = R * 2;
     const int gg = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
@@ -182,6 +189,64 @@ template <int MT>
 FER_DEV typename Acc<MT>::T mfma(bf16x8 a, bf16x8 b, typename Acc<MT>::T c) {
   if constexpr (MT == 32) return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
   else return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// ---- epilogue. Accumulator element (i, j, q, r) -> tile row/col. Split-K partials go to
+// the fp32 slab; otherwise each wave-row half of the tile (in EPC row chunks) is staged
+// through LDS as fp32 with padded rows and every thread applies the epilogue on 4 consecutive
+// columns of one row: all global traffic of the epilogue is row-contiguous.
+template <int BM, int BN, int WM, int WN, int MT, int EPC, typename AccT, int FN, int FM>
+FER_DEV void tile_epilogue(const GemmArgs& g, const EpiArgs& e, AccT (&acc)[FN][FM], char* smem, int m0, int n0,
+                           int ks, int wm, int wn, int lane) {
+  constexpr int TM = BM / WM, TN = BN / WN;
+  constexpr int NQ = MT == 32 ? 4 : 1;
+  const int lr = MT == 32 ? (lane & 31) : (lane & 15);
+  const int lc = MT == 32 ? 4 * (lane >> 5) : 4 * (lane >> 4);
+  if (g.partial) {  // split-K partial slab, fp32 [split][M][N]
+    float* ws = g.ws + (long)ks * g.M * g.N;
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+      for (int j = 0; j < FM; ++j)
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+          const long m = m0 + wm * TM + j * MT + lr, n = n0 + wn * TN + i * MT + 8 * q + lc;
+          if (m < g.M && n < g.N)
+            *(f32x4*)(ws + m * g.N + n) =
+                f32x4{acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]};
+        }
+    return;
+  }
+  static_assert(WM == 2, "epilogue staging splits the tile by the wave-row halves");
+  constexpr int EROWS = TM / EPC, ELD = BN + 4, FJ = FM / EPC;
+  static_assert(FJ * EPC == FM, "row chunks must split the MFMA blocks evenly");
+  float* ep = (float*)smem;
+  constexpr int NT = 64 * WM * WN;
+  constexpr int C4 = BN / 4;  // float4 groups per row
+#pragma unroll
+  for (int h = 0; h < 2 * EPC; ++h) {
+    __syncthreads();
+    if (wm == h / EPC) {
+#pragma unroll
+      for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int jj = 0; jj < FJ; ++jj)
+#pragma unroll
+          for (int q = 0; q < NQ; ++q) {
+            const int j = (h % EPC) * FJ + jj;
+            const int r = jj * MT + lr;
+            const int c = wn * TN + i * MT + 8 * q + lc;
+            *(f32x4*)(ep + r * ELD + c) =
+                f32x4{acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]};
+          }
+    }
+    __syncthreads();
+    for (int idx = threadIdx.x; idx < EROWS * C4; idx += NT) {
+      const int r = idx / C4, c = (idx - r * C4) * 4;
+      const long m = m0 + h * EROWS + r, n = n0 + c;
+      if (m < g.M && n < g.N) epi4<bf16>(e, m, n, *(const f32x4*)(ep + r * ELD + c));
+    }
+  }
 }
 
 // Wave grid WM x WN over a BM x BN tile; each wave owns (BM/WM) x (BN/WN) as MT x MT MFMA
@@ -287,54 +352,301 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g, 
     if (acc[0][0][0] == 12345.f) g.ws[0] = 1.f;  // keep the MFMAs alive
     return;
   }
-  // ---- epilogue. Accumulator element (i, j, q, r) -> tile row/col:
-  constexpr int NQ = MT == 32 ? 4 : 1;
-  const int lr = MT == 32 ? (lane & 31) : (lane & 15);
-  const int lc = MT == 32 ? 4 * (lane >> 5) : 4 * (lane >> 4);
-  if (g.partial) {  // split-K partial slab, fp32 [split][M][N]
-    float* ws = g.ws + (long)ks * g.M * g.N;
+  tile_epilogue<BM, BN, WM, WN, MT, 1>(g, e, acc, smem, m0, n0, ks, wm, wn, lane);
+}
+
+// Ring variant: BK=32 stages in an NST-slot LDS ring, LDS-DMA issued NST-1 K-steps ahead and
+// spread over the substeps (so no wave blocks on a burst of DMA issue and each stage has
+// ~NST-2 K-steps to land). Per K-step t, in its last substep: counted vmcnt for stage t+1,
+// s_barrier, fragment reads of (t+1, 0) — behind the MFMAs of (t, last). The slot refilled in
+// step t is the one read in step t-1, released by the barrier of step t-1... which every wave
+// passed after issuing (and before consuming) those reads.
+template <int BM, int BN, int WM, int WN, bool AKC, bool BKC, int MT, int NST>
+__global__ __launch_bounds__(64 * WM * WN, 1) void gemm_ring_kernel(GemmArgs g, EpiArgs e) {
+  typedef typename Acc<MT>::T AccT;
+  constexpr int RBK = 32;
+  constexpr int NW = WM * WN;
+  constexpr int TM = BM / WM, TN = BN / WN;
+  constexpr int FM = TM / MT, FN = TN / MT;
+  constexpr int SS = MT == 32 ? 2 : 1;
+  constexpr int PD = NST - 1;  // prefetch distance in K-steps
+  constexpr int A_BYTES = BM * RBK * 2, B_BYTES = BN * RBK * 2;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int EPC = (TM * (BN + 4) * 4 <= NST * STAGE) ? 1 : 2;
+  static_assert(TM / EPC * (BN + 4) * 4 <= NST * STAGE, "epilogue staging does not fit");
+  __shared__ __attribute__((aligned(1024))) char smem[NST * STAGE];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave % WM, wn = wave / WM;
+
+  int tm, tn;
+  tile_of(blockIdx.x, g.tiles_m, g.tiles_n, tm, tn);
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int ks = blockIdx.y;
+  const int kbeg = ks * g.k_chunk;
+  const int kend = min(g.K, kbeg + g.k_chunk);
+  const int nk = (kend - kbeg + RBK - 1) / RBK;
+
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(g.A);
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(g.B);
+  typedef DmaPlan<BM, AKC, NW, MT, RBK> PA;
+  typedef DmaPlan<BN, BKC, NW, MT, RBK> PB;
+  PA pa;
+  PB pb;
+  pa.init(wave, lane, g.lda, m0, g.M);
+  pb.init(wave, lane, g.ldb, n0, g.N);
+  const int ktail = kbeg + (nk - 1) * RBK;
+  constexpr int PER = PA::NI + PB::NI;      // DMA instructions per stage per wave
+  constexpr int EARLY = SS > 1 ? PA::NI : 0;  // of those, issued before the last substep
+
+  AccT acc[FN][FM];
 #pragma unroll
-    for (int i = 0; i < FN; ++i)
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int j = 0; j < FM; ++j) acc[i][j] = AccT{};
+
+  auto slot = [&](int st) -> char* { return smem + (st % NST) * STAGE; };
+  auto issue_a = [&](int st) {
+    const int k0 = kbeg + st * RBK;
+    pa.issue(ra, slot(st), wave, g.lda, k0, kend, k0 == ktail);
+  };
+  auto issue_b = [&](int st) {
+    const int k0 = kbeg + st * RBK;
+    pb.issue(rb, slot(st) + A_BYTES, wave, g.ldb, k0, kend, k0 == ktail);
+  };
+
+  bf16x8 af[FM], bfr[FN];
+  if (nk > 0) {
+#pragma unroll
+    for (int st = 0; st < PD; ++st)
+      if (st < nk) {
+        issue_a(st);
+        issue_b(st);
+      }
+    // stage 0 landed: the stages after it may still be in flight
+    if (nk >= 3) wait_vm<2 * PER>();
+    else if (nk == 2) wait_vm<PER>();
+    else wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < FN; ++i) bfr[i] = read_frag<MT, BN, BKC, RBK>(smem + A_BYTES, wn * TN + i * MT, 0, lane);
+#pragma unroll
+    for (int j = 0; j < FM; ++j) af[j] = read_frag<MT, BM, AKC, RBK>(smem, wm * TM + j * MT, 0, lane);
+  }
+  static_assert(NST == 4, "vmcnt bookkeeping below assumes a 4-slot ring (PD = 3)");
+  for (int t = 0; t < nk; ++t) {
+    const char* cur = slot(t);
+    const bool pf = t + PD < nk;
+#pragma unroll
+    for (int kk = 0; kk < SS; ++kk) {
+      bf16x8 an[FM], bn[FN];
+      if (kk < SS - 1) {
+#pragma unroll
+        for (int i = 0; i < FN; ++i) bn[i] = read_frag<MT, BN, BKC, RBK>(cur + A_BYTES, wn * TN + i * MT, kk + 1, lane);
+#pragma unroll
+        for (int j = 0; j < FM; ++j) an[j] = read_frag<MT, BM, AKC, RBK>(cur, wm * TM + j * MT, kk + 1, lane);
+        if (pf) issue_a(t + PD);
+      } else {
+        if (t + 1 < nk) {
+          // stage t+1 landed; stage t+2 and (SS>1) the A pieces of stage t+3 may be in flight
+          if (pf) wait_vm<PER + EARLY>();
+          else if (t + 2 < nk) wait_vm<PER>();
+          else wait_vm<0>();
+          __builtin_amdgcn_s_barrier();
+          asm volatile("" ::: "memory");
+          const char* nx = slot(t + 1);
+#pragma unroll
+          for (int i = 0; i < FN; ++i) bn[i] = read_frag<MT, BN, BKC, RBK>(nx + A_BYTES, wn * TN + i * MT, 0, lane);
+#pragma unroll
+          for (int j = 0; j < FM; ++j) an[j] = read_frag<MT, BM, AKC, RBK>(nx, wm * TM + j * MT, 0, lane);
+        }
+        if (pf) {
+          if (SS == 1) issue_a(t + PD);
+          issue_b(t + PD);
+        }
+      }
 #pragma unroll
       for (int j = 0; j < FM; ++j)
 #pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-          const long m = m0 + wm * TM + j * MT + lr, n = n0 + wn * TN + i * MT + 8 * q + lc;
-          if (m < g.M && n < g.N)
-            *(f32x4*)(ws + m * g.N + n) =
-                f32x4{acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]};
-        }
-    return;
-  }
-  // Stage each half of the tile (the rows of wave-row wm == h) through LDS as fp32 with padded
-  // rows, then every thread applies the epilogue on 4 consecutive columns of one row: all
-  // global traffic of the epilogue (bias, pre, residual, aux, output) is row-contiguous.
-  float* ep = (float*)smem;
-  constexpr int NT = 64 * NW;
-  constexpr int C4 = BN / 4;  // float4 groups per row
+        for (int i = 0; i < FN; ++i) acc[i][j] = mfma<MT>(bfr[i], af[j], acc[i][j]);
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    __syncthreads();
-    if (wm == h) {
+      for (int i = 0; i < FN; ++i) bfr[i] = bn[i];
 #pragma unroll
-      for (int i = 0; i < FN; ++i)
-#pragma unroll
-        for (int j = 0; j < FM; ++j)
-#pragma unroll
-          for (int q = 0; q < NQ; ++q) {
-            const int r = j * MT + lr;
-            const int c = wn * TN + i * MT + 8 * q + lc;
-            *(f32x4*)(ep + r * ELD + c) =
-                f32x4{acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]};
-          }
-    }
-    __syncthreads();
-    for (int idx = threadIdx.x; idx < EROWS * C4; idx += NT) {
-      const int r = idx / C4, c = (idx - r * C4) * 4;
-      const long m = m0 + h * EROWS + r, n = n0 + c;
-      if (m < g.M && n < g.N) epi4<bf16>(e, m, n, *(const f32x4*)(ep + r * ELD + c));
+      for (int j = 0; j < FM; ++j) af[j] = an[j];
     }
   }
+  tile_epilogue<BM, BN, WM, WN, MT, EPC>(g, e, acc, smem, m0, n0, ks, wm, wn, lane);
+}
+
+// ===================================================================== 8-phase kernel
+// 256x256x64 tile, 8 waves as 2 (row halves, wr = wave>>2) x 4 (column quarters, wc = wave&3),
+// each wave a 128x64 accumulator tile cut into four 64x32 quadrants. A K-tile runs as four
+// PHASES; each phase is  [load segment: fragment ds_reads + one 16 KB LDS-DMA unit + counted
+// vmcnt] s_barrier [MFMA segment, s_setprio 1: one quadrant x K=64] s_barrier.  Waves 4-7 run
+// one barrier behind waves 0-3, so on every SIMD one wave's MFMA segment overlaps its
+// partner's load segment and the matrix pipe never waits on LDS/DMA issue.
+//
+// LDS: 2 buffers x {A unit qm=0, A unit qm=1, B unit qn=0, B unit qn=1}, 16 KB each. A unit qm
+// holds the 128 A rows {wr*128 + qm*64 + i}; B unit qn the 128 B columns {wc*64 + qn*32 + i}:
+// exactly what quadrant row/column qm/qn of all waves reads, so a unit is refilled as soon as
+// its readers are done. Quadrant order (0,0) (1,1) (0,1) (1,0): phases 0 and 1 read all
+// fragments (8 A + 4 B each), phases 2 and 3 reuse them. Unit issue per phase q of K-tile T:
+//   q=0: B0(T+1)  q=1: A1(T+1)  q=2: B1(T+1)  q=3: A0(T+2)
+// (each >= 3 phases after its last read in the same buffer). Waits: q=3 retires A0/B0(T+1)
+// (vmcnt 6: A1, B1(T+1), A0(T+2) may fly), q=0 retires A1/B1(T) (vmcnt 4); a unit is read one
+// phase after the wait that retires it (the barrier between publishes other waves' DMA).
+template <bool KC, int MT, bool ISA>
+struct UnitPlan {
+  uint32_t base[2];
+  int kof[2];
+  // local index (0..127) -> index inside the 256-wide tile
+  FER_DEV static int map(int l, int q) {
+    return ISA ? (l >> 6) * 128 + q * 64 + (l & 63) : (l >> 5) * 64 + q * 32 + (l & 31);
+  }
+  FER_DEV void init(int wave, int lane, long ld, int r0, int rmax, int q) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int gi = wave * 2 + i;
+      bool ok;
+      uint32_t off;
+      if constexpr (KC) {
+        const int row = gi * 8 + (lane >> 3);
+        const int c = (lane & 7) ^ kc_swz<64>(row);
+        const int gr = r0 + map(row, q);
+        ok = gr < rmax;
+        kof[i] = c * 8;
+        off = (uint32_t)(((long)gr * ld + c * 8) * 2);
+      } else {
+        const int byte = gi * 1024 + lane * 16;
+        const int k = byte >> 8;
+        const int c = ((byte & 255) >> 4) ^ mn_swz_t<MT>(k);
+        const int gc = r0 + map(c * 8, q);
+        ok = gc < rmax;
+        kof[i] = k;
+        off = (uint32_t)(((long)k * ld + gc) * 2);
+      }
+      base[i] = ok ? off : FER_OOB;
+    }
+  }
+  FER_DEV void issue(__amdgpu_buffer_rsrc_t rs, char* unit, int wave, long ld, int k0, int kmax, bool tail) const {
+    const uint32_t kadd = KC ? (uint32_t)(k0 * 2) : (uint32_t)(k0 * ld * 2);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const uint32_t voff = (!tail || k0 + kof[i] < kmax) ? base[i] + kadd : FER_OOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(unit + (wave * 2 + i) * 1024), 16, voff, 0, 0, 0);
+    }
+  }
+};
+
+template <bool AKC, bool BKC, int MT>
+__global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmArgs g, EpiArgs e) {
+  typedef typename Acc<MT>::T AccT;
+  constexpr int UNIT = 16384, BUF = 4 * UNIT;  // A0 A1 B0 B1
+  constexpr int FM = 128 / MT, FN = 64 / MT;   // MFMA blocks per wave (rows, cols)
+  constexpr int QJ = FM / 2, QI = FN / 2;      // per quadrant
+  constexpr int KS = 64 / (MT == 32 ? 16 : 32);  // MFMA K-steps per K-tile
+  __shared__ __attribute__((aligned(1024))) char smem[2 * BUF];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+
+  int tm, tn;
+  tile_of(blockIdx.x, g.tiles_m, g.tiles_n, tm, tn);
+  const int m0 = tm * 256, n0 = tn * 256;
+  const int ks = blockIdx.y;
+  const int kbeg = ks * g.k_chunk;
+  const int kend = min(g.K, kbeg + g.k_chunk);
+  const int nk = (kend - kbeg + 63) / 64;
+  const int ktail = kbeg + (nk - 1) * 64;
+
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(g.A);
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(g.B);
+  UnitPlan<AKC, MT, true> pa0, pa1;
+  UnitPlan<BKC, MT, false> pb0, pb1;
+  pa0.init(wave, lane, g.lda, m0, g.M, 0);
+  pa1.init(wave, lane, g.lda, m0, g.M, 1);
+  pb0.init(wave, lane, g.ldb, n0, g.N, 0);
+  pb1.init(wave, lane, g.ldb, n0, g.N, 1);
+  auto unit = [&](int T, int u) -> char* { return smem + (T & 1) * BUF + u * UNIT; };
+  auto kt = [&](int T) { return kbeg + T * 64; };
+  auto iA0 = [&](int T) { pa0.issue(ra, unit(T, 0), wave, g.lda, kt(T), kend, kt(T) == ktail); };
+  auto iA1 = [&](int T) { pa1.issue(ra, unit(T, 1), wave, g.lda, kt(T), kend, kt(T) == ktail); };
+  auto iB0 = [&](int T) { pb0.issue(rb, unit(T, 2), wave, g.ldb, kt(T), kend, kt(T) == ktail); };
+  auto iB1 = [&](int T) { pb1.issue(rb, unit(T, 3), wave, g.ldb, kt(T), kend, kt(T) == ktail); };
+
+  AccT acc[FN][FM];
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int j = 0; j < FM; ++j) acc[i][j] = AccT{};
+  bf16x8 fa[2][KS][QJ], fb[2][KS][QI];
+
+  if (nk > 0) {
+    iA0(0); iB0(0); iA1(0); iB1(0);
+    if (nk > 1) {
+      iA0(1);
+      wait_vm<6>();
+    } else {
+      wait_vm<4>();
+    }
+    __builtin_amdgcn_s_barrier();
+    if (wr) __builtin_amdgcn_s_barrier();  // stagger: waves 4-7 one barrier behind
+    asm volatile("" ::: "memory");
+  }
+
+  for (int T = 0; T < nk; ++T) {
+    const bool n1 = T + 1 < nk, n2 = T + 2 < nk;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      // ---- load segment
+      if (q < 2) {
+        const char* ua = unit(T, q);
+        const char* ub = unit(T, 2 + q);
+#pragma unroll
+        for (int kk = 0; kk < KS; ++kk)
+#pragma unroll
+          for (int i = 0; i < QI; ++i) fb[q][kk][i] = read_frag<MT, 128, BKC, 64>(ub, wc * 32 + i * MT, kk, lane);
+#pragma unroll
+        for (int kk = 0; kk < KS; ++kk)
+#pragma unroll
+          for (int j = 0; j < QJ; ++j) fa[q][kk][j] = read_frag<MT, 128, AKC, 64>(ua, wr * 64 + j * MT, kk, lane);
+      }
+      if (q == 0) {
+        if (n1) { iB0(T + 1); wait_vm<4>(); } else { wait_vm<0>(); }
+      } else if (q == 1) {
+        if (n1) iA1(T + 1);
+      } else if (q == 2) {
+        if (n1) iB1(T + 1);
+      } else {
+        if (n2) { iA0(T + 2); wait_vm<6>(); } else if (n1) { wait_vm<4>(); }
+      }
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      // ---- MFMA segment: quadrant (qm, qn) for q = 0..3 -> (0,0) (1,1) (0,1) (1,0)
+      constexpr int dummy = 0;
+      (void)dummy;
+      const int qm = (q == 0 || q == 2) ? 0 : 1;
+      const int qn = (q == 0 || q == 3) ? 0 : 1;
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int kk = 0; kk < KS; ++kk)
+#pragma unroll
+        for (int j = 0; j < QJ; ++j)
+#pragma unroll
+          for (int i = 0; i < QI; ++i)
+            acc[qn * QI + i][qm * QJ + j] = mfma<MT>(fb[qn][kk][i], fa[qm][kk][j], acc[qn * QI + i][qm * QJ + j]);
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
+  }
+  if (nk > 0 && !wr) __builtin_amdgcn_s_barrier();  // waves 0-3 catch up with the stagger
+  static_assert(64 * (256 + 4) * 4 <= 2 * BUF, "epilogue staging (2 chunks per half) must fit");
+  tile_epilogue<256, 256, 2, 4, MT, 2>(g, e, acc, smem, m0, n0, ks, wr, wc, lane);
 }
 
 // Ordered (deterministic) split-K reduction + epilogue.
@@ -403,30 +715,52 @@ static int launch_bf16(GemmArgs g, const EpiArgs& e, hipStream_t st) {
   return 0;
 }
 
-static int forced_cfg() {
-  static int v = -2;
-  if (v == -2) {
-    const char* s = getenv("FERVIT_GEMM_CFG");
-    v = s ? atoi(s) : -1;
-  }
-  return v;
+template <int BM, int BN, int WM, int WN, bool AKC, bool BKC, int MT>
+static int launch_ring(GemmArgs g, const EpiArgs& e, hipStream_t st) {
+  g.tiles_m = (g.M + BM - 1) / BM;
+  g.tiles_n = (g.N + BN - 1) / BN;
+  dim3 grid(g.tiles_m * g.tiles_n, g.splits);
+  hipLaunchKernelGGL((gemm_ring_kernel<BM, BN, WM, WN, AKC, BKC, MT, 4>), grid, dim3(64 * WM * WN), 0, st, g, e);
+  return 0;
 }
 
+template <bool AKC, bool BKC, int MT>
+static int launch_8ph(GemmArgs g, const EpiArgs& e, hipStream_t st) {
+  g.tiles_m = (g.M + 255) / 256;
+  g.tiles_n = (g.N + 255) / 256;
+  dim3 grid(g.tiles_m * g.tiles_n, g.splits);
+  hipLaunchKernelGGL((gemm_8ph_kernel<AKC, BKC, MT>), grid, dim3(512), 0, st, g, e);
+  return 0;
+}
+
+static int g_forced_cfg = -2;  // -2: read FERVIT_GEMM_CFG once; -1: automatic
+
+static int forced_cfg() {
+  if (g_forced_cfg == -2) {
+    const char* s = getenv("FERVIT_GEMM_CFG");
+    g_forced_cfg = s ? atoi(s) : -1;
+  }
+  return g_forced_cfg;
+}
+
+// Tile configuration: 0..3 double-buffered (256^2 MT32, 256^2 MT16, 128^2 MT32, 128^2 MT16),
+// 4..7 BK=32 ring (same order), 8/9 the 8-phase 256^2 kernel (MT16 / MT32).
+static bool cfg_is_256(int c) { return c == 0 || c == 1 || c == 4 || c == 5 || c == 8 || c == 9; }
+
 template <bool AKC, bool BKC>
-static int dispatch_tile(GemmArgs g, const EpiArgs& e, hipStream_t st) {
-  switch (forced_cfg()) {
+static int dispatch_tile(int cfg, GemmArgs g, const EpiArgs& e, hipStream_t st) {
+  switch (cfg) {
     case 0: return launch_bf16<256, 256, 2, 4, AKC, BKC, 32>(g, e, st);
     case 1: return launch_bf16<256, 256, 2, 4, AKC, BKC, 16>(g, e, st);
     case 2: return launch_bf16<128, 128, 2, 2, AKC, BKC, 32>(g, e, st);
     case 3: return launch_bf16<128, 128, 2, 2, AKC, BKC, 16>(g, e, st);
-    default: break;
+    case 4: return launch_ring<256, 256, 2, 4, AKC, BKC, 32>(g, e, st);
+    case 5: return launch_ring<256, 256, 2, 4, AKC, BKC, 16>(g, e, st);
+    case 6: return launch_ring<128, 128, 2, 2, AKC, BKC, 32>(g, e, st);
+    case 7: return launch_ring<128, 128, 2, 2, AKC, BKC, 16>(g, e, st);
+    case 9: return launch_8ph<AKC, BKC, 32>(g, e, st);
+    default: return launch_8ph<AKC, BKC, 16>(g, e, st);
   }
-  // measured on MI355X (tools/gemm_bench.py): 256^2 / 8 waves / 32x32x16 for the forward and
-  // dgrad layouts when the grid fills the chip; 128^2 / 4 waves / 16x16x32 (2 blocks per CU)
-  // for split-K weight gradients and small problems.
-  const long t256 = ((g.M + 255) / 256) * ((g.N + 255) / 256) * (long)g.splits;
-  if (AKC && t256 >= 200) return launch_bf16<256, 256, 2, 4, AKC, BKC, 32>(g, e, st);
-  return launch_bf16<128, 128, 2, 2, AKC, BKC, 16>(g, e, st);
 }
 
 int gemm_launch(const GemmDesc& d, const EpiArgs& e_in, hipStream_t st) {
@@ -454,25 +788,30 @@ int gemm_launch(const GemmDesc& d, const EpiArgs& e_in, hipStream_t st) {
   const long b_bytes = (d.b_kc ? (long)(d.N - 1) * d.ldb + d.K : (long)(d.K - 1) * d.ldb + d.N) * 2;
   if (a_bytes >= 0x7FFFFFF0L || b_bytes >= 0x7FFFFFF0L) return set_error("gemm: operand exceeds 2 GiB");
 
-  // split-K when the output tiles alone cannot fill 256 CUs
-  int splits = 1;
-  const long tiles = ((d.M + 255) / 256) * ((d.N + 255) / 256);
-  const long tiles128 = ((d.M + 127) / 128) * ((d.N + 127) / 128);
-  if (d.ws && tiles < 200 && tiles128 < 256 && d.K >= 1024) {
-    const long t = tiles128;
-    splits = (int)std::min<long>((512 + t - 1) / t, d.K / 256);
-    splits = std::max(1, std::min<int>(splits, (int)(d.ws_bytes / ((long)d.M * d.N * 4))));
-  }
+  // Configuration (measured on MI355X, tools/gemm_bench.py): the 8-phase 256^2 kernel whenever
+  // the grid (with split-K) gives it >= 128 workgroups (the BK=32 ring for the MN x MN weight
+  // gradient: 261 vs 283 us on fc1), else 128^2 tiles at 2 blocks per CU.
+  // Split-K (weight gradients, K = tokens) targets one 256^2 workgroup per CU.
+  const long t256 = (long)((d.M + 255) / 256) * ((d.N + 255) / 256);
+  const long t128 = (long)((d.M + 127) / 128) * ((d.N + 127) / 128);
+  const int max_splits = d.ws ? (int)std::min<long>(64, d.ws_bytes / ((long)d.M * d.N * 4)) : 1;
+  auto splits_for = [&](long tiles, long target) -> int {
+    if (max_splits < 2 || d.K < 1024 || tiles >= target) return 1;
+    return (int)std::max<long>(1, std::min<long>({target / tiles, d.K / 256, (long)max_splits}));
+  };
+  int cfg = forced_cfg();
+  if (cfg < 0) cfg = t256 * splits_for(t256, 256) >= 128 ? (!d.a_kc && !d.b_kc ? 5 : 8) : 3;
+  int splits = cfg_is_256(cfg) ? splits_for(t256, 256) : splits_for(t128, 512);
   g.splits = splits;
   g.k_chunk = splits > 1 ? (((d.K + splits - 1) / splits + BK - 1) / BK) * BK : d.K;
   if (splits > 1) g.splits = (d.K + g.k_chunk - 1) / g.k_chunk;
   g.partial = g.splits > 1;
   g.ws = d.ws;
 
-  if (d.a_kc && d.b_kc) dispatch_tile<true, true>(g, e, st);
-  else if (d.a_kc && !d.b_kc) dispatch_tile<true, false>(g, e, st);
-  else if (!d.a_kc && !d.b_kc) dispatch_tile<false, false>(g, e, st);
-  else dispatch_tile<false, true>(g, e, st);
+  if (d.a_kc && d.b_kc) dispatch_tile<true, true>(cfg, g, e, st);
+  else if (d.a_kc && !d.b_kc) dispatch_tile<true, false>(cfg, g, e, st);
+  else if (!d.a_kc && !d.b_kc) dispatch_tile<false, false>(cfg, g, e, st);
+  else dispatch_tile<false, true>(cfg, g, e, st);
   int rc = hip_check("gemm_bf16");
   if (rc || !g.partial) return rc;
   const long work = (long)d.M * (d.N / 4);
@@ -483,3 +822,9 @@ int gemm_launch(const GemmDesc& d, const EpiArgs& e_in, hipStream_t st) {
 }
 
 }  // namespace fer
+
+extern "C" int fer_gemm_set_config(int cfg) {
+  if (cfg < -1 || cfg > 9) return fer::set_error("gemm_set_config: cfg must be -1 (automatic) or 0..9");
+  fer::g_forced_cfg = cfg;
+  return 0;
+}

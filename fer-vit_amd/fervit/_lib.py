@@ -40,6 +40,7 @@ class AdamWSegment(C.Structure):
 # name -> (restype, argtypes)
 SIGNATURES = {
     "fer_gemm": (i32, [C.POINTER(GemmDesc), C.POINTER(Epilogue), vp]),
+    "fer_gemm_set_config": (i32, [i32]),
     "fer_layernorm_fwd": (i32, [i32, vp, i64, fp, fp, i32, i32, vp, i64, fp, fp, i32, i32, f32, vp]),
     "fer_layernorm_bwd_ws": (i64, [i32, i32]),
     "fer_layernorm_bwd": (i32, [i32, vp, i64, vp, i64, fp, fp, fp, i32, i32, vp, i64, vp, i64, vp, u32, f32, u64,

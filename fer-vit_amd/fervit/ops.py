@@ -89,8 +89,10 @@ def gemm(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, *, a_kc: bool = Tr
     d.ldb = ldb if ldb is not None else (K if b_kc else N)
     d.a_kc, d.b_kc = int(a_kc), int(b_kc)
     d.M, d.N, d.K = M, N, K
-    if split_ws and d.dtype == 0:
-        nb = 4 * M * N * 8
+    t256 = -(-M // 256) * -(-N // 256)
+    if split_ws and d.dtype == 0 and K >= 1024 and t256 < 256:
+        # split-K slabs: the library targets ~one 256x256 workgroup per CU (or 512 128^2 ones)
+        nb = 4 * M * N * min(32, max(2, 512 // t256))
         w = WS.get(nb, A.device, slot=1)
         d.ws, d.ws_bytes = w.data_ptr(), w.numel() * 4
     e = Epilogue()

@@ -62,6 +62,11 @@ typedef struct {
 
 int fer_gemm(const fer_gemm_desc* d, const fer_epilogue* e, fer_stream_t stream);
 
+/* Tuning/testing hook (no reference counterpart): force the bf16 GEMM tile configuration for
+ * every later fer_gemm call of the process. -1 = automatic (default); 0..9 = fixed kernel
+ * (see csrc/gemm.hip). Results are identical up to fp32 summation order. */
+int fer_gemm_set_config(int cfg);
+
 /* LayerNorm forward over rows of x [M][D] (nn.LayerNorm, biased variance;
  * post-norm `nn.TransformerEncoderLayer` norm1/norm2, heads `image_vit.py:162-163`,
  * `latent_vit.py:33-36`, timm pre-norm eps 1e-6). gamma/beta are [gamma_rows][D]:

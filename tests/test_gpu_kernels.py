@@ -56,6 +56,32 @@ def test_linear_fwd_dgrad_wgrad(M, N, K, dtype):
     assert rel_err(gw.cpu(), 2 * (dyr.t() @ xr)) < tol
 
 
+@pytest.mark.parametrize("cfg", list(range(10)))
+def test_gemm_every_tile_config(cfg):
+    """Each bf16 kernel configuration (forced through fer_gemm_set_config) on ragged shapes,
+    all three operand layouts, split-K, and the fused epilogue."""
+    from fervit._lib import lib
+
+    o = ops()
+    lib().fer_gemm_set_config(cfg)
+    try:
+        for M, N, K in [(300, 136, 200), (777, 520, 1096), (2056, 264, 520)]:
+            g = torch.Generator().manual_seed(M + cfg)
+            x = torch.randn(M, K, generator=g)
+            w = torch.randn(N, K, generator=g) / math.sqrt(K)
+            dy = torch.randn(M, N, generator=g)
+            b = torch.randn(N, generator=g)
+            xr, wr, dyr = (bf(t).float().cpu().double() for t in (x, w, dy))
+            y = o.linear_fwd(bf(x), bf(w), b.to(DEV), act="relu")
+            assert rel_err(y.cpu(), torch.relu(xr @ wr.t() + b.double())) < 1e-2, (cfg, M, N, K)
+            assert rel_err(o.linear_dgrad(bf(dy), bf(w)).cpu(), dyr @ wr) < 1e-2, (cfg, M, N, K)
+            gw = torch.zeros(N, K, device=DEV)
+            o.linear_wgrad(bf(dy), bf(x), gw)
+            assert rel_err(gw.cpu(), dyr.t() @ xr) < 1e-2, (cfg, M, N, K)
+    finally:
+        lib().fer_gemm_set_config(-1)
+
+
 @pytest.mark.parametrize("act", ["gelu", "relu"])
 def test_gemm_epilogue_bias_act_dropout_residual(act):
     o = ops()
