@@ -70,231 +70,314 @@ FER_DEV f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) { return __builtin_amdgcn_mf
 // accumulator register -> row within the 32-row tile
 FER_DEV int acc_row(int reg, int hh) { return (reg & 3) + 8 * (reg >> 2) + 4 * hh; }
 
+// Dropout element index of P[bh][q][k]: (bh*N + q)*NP + k with NP = N rounded up to even, so
+// keys 2j, 2j+1 of one query share one 32-bit hash (one 16-bit half each).
+FER_DEV uint64_t drop_row(int bh, int N, int q) { return ((uint64_t)bh * N + q) * (uint64_t)(N + (N & 1)); }
+
+// Keep flags of the 16 accumulator registers when registers hold KEYS (S^T orientation:
+// registers 2i, 2i+1 are consecutive keys, first one even): 8 hashes per lane.
+FER_DEV uint32_t keep16_keys(uint64_t seed, uint64_t row, int kb, int hh, uint32_t thr) {
+  uint32_t bits = 0;
+#pragma unroll
+  for (int r = 0; r < 16; r += 2) {
+    const uint32_t h = fer_hash(seed, (row + kb * 32 + acc_row(r, hh)) >> 1);
+    bits |= (uint32_t)((h & 0xFFFFu) >= thr) << r;
+    bits |= (uint32_t)((h >> 16) >= thr) << (r + 1);
+  }
+  return bits;
+}
+
+// rows [0, 32*NB) of a [N][dh] column block -> swizzled LDS image by LDS-DMA (16 B per lane,
+// lane-linear destination, swizzle applied on the source address). Wave w of NB issues the
+// four 1 KB pieces [4w, 4w+4). Rows >= N and chunks >= dh/8 are zero-filled (range check).
 template <int NB>
-__global__ __launch_bounds__(64 * NB) void attn_fwd_bf16(const bf16* __restrict__ qkv, long ldq, bf16* __restrict__ out,
-                                                       long ldo, float* __restrict__ lse, int N, int H, int dh,
-                                                       float sl2, uint32_t thr, float dscale, uint64_t seed) {
-  __shared__ __attribute__((aligned(16))) char lds[2 * NB * 32 * 128];
+FER_DEV void img_dma(char* img, __amdgpu_buffer_rsrc_t rs, long row0, long ld, int col0, int N, int dh, int w,
+                     int lane) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int pc = 4 * w + i;
+    const int r = pc * 8 + (lane >> 3);
+    const int ch = (lane & 7) ^ swz(r);
+    const bool ok = r < N && ch * 8 < dh;
+    const uint32_t voff = ok ? (uint32_t)(((row0 + r) * ld + col0 + ch * 8) * 2) : FER_OOB;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(img + pc * 1024), 16, voff, 0, 0, 0);
+  }
+}
+
+FER_DEV void store_rows_q(bf16* o, const f32x16 (&acc)[2], float mul, int hh, int dh) {
+#pragma unroll
+  for (int db = 0; db < 2; ++db)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const int d = db * 32 + 8 * g4 + 4 * hh;
+      if (d < dh)
+        *(bf16x4*)(o + d) = bf16x4{(bf16)(acc[db][4 * g4] * mul), (bf16)(acc[db][4 * g4 + 1] * mul),
+                                   (bf16)(acc[db][4 * g4 + 2] * mul), (bf16)(acc[db][4 * g4 + 3] * mul)};
+    }
+}
+
+// ---------------------------------------------------------------- forward
+// One workgroup per (batch, head), wave w = query block w. K and V images arrive by LDS-DMA;
+// S^T = K Q^T per 32-key block with an online (running max) softmax, O^T += V^T P^T.
+template <int NB>
+__global__ __launch_bounds__(64 * NB) __attribute__((amdgpu_waves_per_eu(4))) void attn_fwd_bf16(const bf16* __restrict__ qkv, long ldq, bf16* __restrict__ out,
+                                                          long ldo, float* __restrict__ lse, int N, int H, int dh,
+                                                          float sl2, uint32_t thr, float dscale, uint64_t seed) {
+  __shared__ __attribute__((aligned(1024))) char lds[2 * NB * 32 * 128];
   char* Ki = lds;
   char* Vi = lds + NB * 32 * 128;
   const int bh = blockIdx.x, b = bh / H, h = bh - b * H, D = H * dh;
-  const bf16* base = qkv + (long)b * N * ldq;
-  load_image<NB>(Ki, base + D + h * dh, ldq, N, dh);
-  load_image<NB>(Vi, base + 2 * D + h * dh, ldq, N, dh);
-
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hh = lane >> 5;
+  const __amdgpu_buffer_rsrc_t rs = make_rsrc(qkv);
+  img_dma<NB>(Ki, rs, (long)b * N, ldq, D + h * dh, N, dh, w, lane);
+  img_dma<NB>(Vi, rs, (long)b * N, ldq, 2 * D + h * dh, N, dh, w, lane);
+
   const int q = w * 32 + (lane & 31);
+  const bf16* base = qkv + (long)b * N * ldq;
   bf16x8 qf[4];
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
     const int d0 = 16 * s + 8 * hh;
     qf[s] = (q < N && d0 < dh) ? *(const bf16x8*)(base + (long)q * ldq + h * dh + d0) : bf16x8{};
   }
-  __syncthreads();
+  __syncthreads();  // vmcnt(0) + barrier: every wave's DMA pieces have landed
 
-  f32x16 st[NB];
-#pragma unroll
+  const uint64_t row = drop_row(bh, N, q);
+  float m = -INFINITY, l = 0.f;
+  f32x16 ot[2] = {f32x16{}, f32x16{}};
+#pragma unroll 1
   for (int kb = 0; kb < NB; ++kb) {
-    st[kb] = f32x16{};
+    f32x16 st = {};
 #pragma unroll
-    for (int s = 0; s < 4; ++s) st[kb] = mfma32(rd_row(Ki, kb * 32 + (lane & 31), 2 * s + hh), qf[s], st[kb]);
-  }
-  float mx = -INFINITY;
-#pragma unroll
-  for (int kb = 0; kb < NB; ++kb)
+    for (int s = 0; s < 4; ++s) st = mfma32(rd_row(Ki, kb * 32 + (lane & 31), 2 * s + hh), qf[s], st);
+    float bm = -INFINITY;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int key = kb * 32 + acc_row(r, hh);
-      const float v = key < N ? st[kb][r] * sl2 : -INFINITY;
-      st[kb][r] = v;
-      mx = fmaxf(mx, v);
+      st[r] = key < N ? st[r] * sl2 : -INFINITY;
+      bm = fmaxf(bm, st[r]);
     }
-  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-  float l = 0.f;
-  const uint64_t rowidx = ((uint64_t)bh * N + q) * (uint64_t)N;
+    bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
+    const float mn = fmaxf(m, bm);
+    const float al = exp2f(m - mn);
+    m = mn;
+    l *= al;
 #pragma unroll
-  for (int kb = 0; kb < NB; ++kb)
+    for (int db = 0; db < 2; ++db) ot[db] *= al;
+    const uint32_t keep = thr ? keep16_keys(seed, row, kb, hh, thr) : 0xFFFFu;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const float e = exp2f(st[kb][r] - mx);
+      const float e = exp2f(st[r] - mn);
       l += e;
-      float pv = e;
-      if (thr) {
-        const int key = kb * 32 + acc_row(r, hh);
-        pv = drop_keep(seed, rowidx + key, thr) ? e * dscale : 0.f;
-      }
-      st[kb][r] = pv;
+      st[r] = thr ? ((keep >> r) & 1 ? e * dscale : 0.f) : e;
     }
-  l += __shfl_xor(l, 32, 64);
-
-  f32x16 ot[2] = {f32x16{}, f32x16{}};
-#pragma unroll
-  for (int kb = 0; kb < NB; ++kb)
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
-      const bf16x8 pf = pack8(st[kb], s2);
+      const bf16x8 pf = pack8(st, s2);
 #pragma unroll
       for (int db = 0; db < 2; ++db) ot[db] = mfma32(rd_tr(Vi, kb * 32 + 16 * s2, db * 32, lane), pf, ot[db]);
     }
+  }
+  l += __shfl_xor(l, 32, 64);
   if (q < N) {
-    const float inv = 1.f / l;
-    bf16* o = out + ((long)b * N + q) * ldo + h * dh;
-#pragma unroll
-    for (int db = 0; db < 2; ++db)
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const int d = db * 32 + 8 * g4 + 4 * hh;
-        if (d < dh)
-          *(bf16x4*)(o + d) = bf16x4{(bf16)(ot[db][4 * g4] * inv), (bf16)(ot[db][4 * g4 + 1] * inv),
-                                     (bf16)(ot[db][4 * g4 + 2] * inv), (bf16)(ot[db][4 * g4 + 3] * inv)};
-      }
-    if (hh == 0) lse[(long)bh * N + q] = (mx + log2f(l)) * LN2;
+    store_rows_q(out + ((long)b * N + q) * ldo + h * dh, ot, 1.f / l, hh, dh);
+    if (hh == 0) lse[(long)bh * N + q] = (m + log2f(l)) * LN2;
   }
 }
 
+// ---------------------------------------------------------------- backward, dQ
+// Wave w = query block w; K, V images by LDS-DMA. Per key block: S^T, dP^T = V dO^T,
+// dS^T = P^T o (dropout'(dP^T) - Dq), dQ^T += K^T dS^T.   Dq = rowsum(dO o O) per query.
 template <int NB>
-__global__ __launch_bounds__(64 * NB) void attn_bwd_bf16(const bf16* __restrict__ qkv, long ldq,
-                                                       const bf16* __restrict__ out, long ldo,
-                                                       const bf16* __restrict__ dout, long lddo,
-                                                       const float* __restrict__ lse, bf16* __restrict__ dqkv,
-                                                       long lddq, int N, int H, int dh, float scale, float sl2,
-                                                       uint32_t thr, float dscale, uint64_t seed) {
+__global__ __launch_bounds__(64 * NB) __attribute__((amdgpu_waves_per_eu(4))) void attn_dq_bf16(const bf16* __restrict__ qkv, long ldq,
+                                                         const bf16* __restrict__ out, long ldo,
+                                                         const bf16* __restrict__ dout, long lddo,
+                                                         const float* __restrict__ lse, bf16* __restrict__ dqkv,
+                                                         long lddq, int N, int H, int dh, float scale, float sl2,
+                                                         uint32_t thr, float dscale, uint64_t seed) {
+  __shared__ __attribute__((aligned(1024))) char lds[2 * NB * 32 * 128];
+  char* Ki = lds;
+  char* Vi = lds + NB * 32 * 128;
+  const int bh = blockIdx.x, b = bh / H, h = bh - b * H, D = H * dh;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hh = lane >> 5;
+  const __amdgpu_buffer_rsrc_t rs = make_rsrc(qkv);
+  img_dma<NB>(Ki, rs, (long)b * N, ldq, D + h * dh, N, dh, w, lane);
+  img_dma<NB>(Vi, rs, (long)b * N, ldq, 2 * D + h * dh, N, dh, w, lane);
+
+  const int q = w * 32 + (lane & 31);
+  const bool qv = q < N;
+  bf16x8 qf[4], of[4];
+  float dsum = 0.f;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int d0 = 16 * s + 8 * hh;
+    const bool ok = qv && d0 < dh;
+    qf[s] = ok ? *(const bf16x8*)(qkv + ((long)b * N + q) * ldq + h * dh + d0) : bf16x8{};
+    of[s] = ok ? *(const bf16x8*)(dout + ((long)b * N + q) * lddo + h * dh + d0) : bf16x8{};
+    const bf16x8 ov = ok ? *(const bf16x8*)(out + ((long)b * N + q) * ldo + h * dh + d0) : bf16x8{};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dsum += (float)ov[j] * (float)of[s][j];
+  }
+  dsum += __shfl_xor(dsum, 32, 64);
+  const float lq = qv ? lse[(long)bh * N + q] * LOG2E : INFINITY;
+  __syncthreads();
+
+  const uint64_t row = drop_row(bh, N, q);
+  f32x16 dqt[2] = {f32x16{}, f32x16{}};
+#pragma unroll 1
+  for (int kb = 0; kb < NB; ++kb) {
+    f32x16 st = {}, dp = {};
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      st = mfma32(rd_row(Ki, kb * 32 + (lane & 31), 2 * s + hh), qf[s], st);
+      dp = mfma32(rd_row(Vi, kb * 32 + (lane & 31), 2 * s + hh), of[s], dp);
+    }
+    const uint32_t keep = thr ? keep16_keys(seed, row, kb, hh, thr) : 0xFFFFu;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int key = kb * 32 + acc_row(r, hh);
+      const float p = key < N ? exp2f(st[r] * sl2 - lq) : 0.f;
+      const float g = thr ? ((keep >> r) & 1 ? dp[r] * dscale : 0.f) : dp[r];
+      st[r] = p * (g - dsum);
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const bf16x8 df = pack8(st, s2);
+#pragma unroll
+      for (int db = 0; db < 2; ++db) dqt[db] = mfma32(rd_tr(Ki, kb * 32 + 16 * s2, db * 32, lane), df, dqt[db]);
+    }
+  }
+  if (qv) store_rows_q(dqkv + ((long)b * N + q) * lddq + h * dh, dqt, scale, hh, dh);
+}
+
+// ---------------------------------------------------------------- backward, dK dV
+// Wave w = key block w; Q and dO images by LDS-DMA, lse and Dq in LDS. Per query block:
+// S = Q K^T, dP = dO V^T (registers hold queries), dV += P_drop^T dO, dK += dS^T Q.
+// The dropout hash pairs are consecutive KEYS = neighbouring lanes here: each lane of a pair
+// hashes 8 of the 16 query rows and swaps them with its neighbour.
+template <int NB>
+__global__ __launch_bounds__(64 * NB) void attn_dkv_bf16(const bf16* __restrict__ qkv, long ldq,
+                                                          const bf16* __restrict__ out, long ldo,
+                                                          const bf16* __restrict__ dout, long lddo,
+                                                          const float* __restrict__ lse, bf16* __restrict__ dqkv,
+                                                          long lddq, int N, int H, int dh, float scale, float sl2,
+                                                          uint32_t thr, float dscale, uint64_t seed) {
   constexpr int IMG = NB * 32 * 128;
-  __shared__ __attribute__((aligned(16))) char lds[4 * IMG + 2 * NB * 32 * 4];
+  __shared__ __attribute__((aligned(1024))) char lds[2 * IMG + 2 * NB * 32 * 4];
   char* Qi = lds;
-  char* Ki = lds + IMG;
-  char* Vi = lds + 2 * IMG;
-  char* Oi = lds + 3 * IMG;  // dO image
-  float* lse_s = (float*)(lds + 4 * IMG);
+  char* Oi = lds + IMG;  // dO image
+  float* lse_s = (float*)(lds + 2 * IMG);
   float* dd_s = lse_s + NB * 32;
   const int bh = blockIdx.x, b = bh / H, h = bh - b * H, D = H * dh;
-  const bf16* base = qkv + (long)b * N * ldq;
-  load_image<NB>(Qi, base + h * dh, ldq, N, dh);
-  load_image<NB>(Ki, base + D + h * dh, ldq, N, dh);
-  load_image<NB>(Vi, base + 2 * D + h * dh, ldq, N, dh);
-  load_image<NB>(Oi, dout + (long)b * N * lddo + h * dh, lddo, N, dh);
-  for (int q = threadIdx.x; q < NB * 32; q += blockDim.x) {
-    float dsum = 0.f, lv = INFINITY;
-    if (q < N) {
-      const bf16* po = out + ((long)b * N + q) * ldo + h * dh;
-      const bf16* pd = dout + ((long)b * N + q) * lddo + h * dh;
-      for (int d = 0; d < dh; d += 8) {
-        bf16x8 a = *(const bf16x8*)(po + d), c = *(const bf16x8*)(pd + d);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hh = lane >> 5;
+  img_dma<NB>(Qi, make_rsrc(qkv), (long)b * N, ldq, h * dh, N, dh, w, lane);
+  img_dma<NB>(Oi, make_rsrc(dout), (long)b * N, lddo, h * dh, N, dh, w, lane);
+
+  // Dq = rowsum(dO o O): two threads per query row
+  for (int t = threadIdx.x; t < NB * 64; t += 64 * NB) {
+    const int qr = t >> 1, half = t & 1;
+    float dsum = 0.f;
+    if (qr < N) {
+      const bf16* po = out + ((long)b * N + qr) * ldo + h * dh;
+      const bf16* pd = dout + ((long)b * N + qr) * lddo + h * dh;
+      for (int d = half * 8; d < dh; d += 16) {
+        const bf16x8 a = *(const bf16x8*)(po + d), c = *(const bf16x8*)(pd + d);
 #pragma unroll
         for (int j = 0; j < 8; ++j) dsum += (float)a[j] * (float)c[j];
       }
-      lv = lse[(long)bh * N + q] * LOG2E;
     }
-    lse_s[q] = lv;
-    dd_s[q] = dsum;
+    dsum += __shfl_xor(dsum, 1, 64);
+    if (!half) {
+      dd_s[qr] = dsum;
+      lse_s[qr] = qr < N ? lse[(long)bh * N + qr] * LOG2E : INFINITY;
+    }
+  }
+  const int key = w * 32 + (lane & 31);
+  const bool kval = key < N;
+  bf16x8 kf[4], vf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int d0 = 16 * s + 8 * hh;
+    const bool ok = kval && d0 < dh;
+    kf[s] = ok ? *(const bf16x8*)(qkv + ((long)b * N + key) * ldq + D + h * dh + d0) : bf16x8{};
+    vf[s] = ok ? *(const bf16x8*)(qkv + ((long)b * N + key) * ldq + 2 * D + h * dh + d0) : bf16x8{};
   }
   __syncthreads();
 
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hh = lane >> 5;
-  // ---------------- phase 1: wave w owns query block w -> dQ
-  {
-    const int q = w * 32 + (lane & 31);
-    bf16x8 qf[4], of[4];
+  const int NP = N + (N & 1);
+  const bool odd = lane & 1;
+  f32x16 dk[2] = {f32x16{}, f32x16{}}, dv[2] = {f32x16{}, f32x16{}};
+#pragma unroll
+  for (int qb = 0; qb < NB; ++qb) {
+    f32x16 st = {}, dp = {};
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      qf[s] = rd_row(Qi, q, 2 * s + hh);
-      of[s] = rd_row(Oi, q, 2 * s + hh);
+      st = mfma32(rd_row(Qi, qb * 32 + (lane & 31), 2 * s + hh), kf[s], st);
+      dp = mfma32(rd_row(Oi, qb * 32 + (lane & 31), 2 * s + hh), vf[s], dp);
     }
-    const float lq = lse_s[q], dq = dd_s[q];
-    const uint64_t rowidx = ((uint64_t)bh * N + q) * (uint64_t)N;
-    f32x16 dqt[2] = {f32x16{}, f32x16{}};
-    for (int kb = 0; kb < NB; ++kb) {
-      f32x16 st = {}, dp = {};
+    uint32_t keep = 0xFFFFu;
+    if (thr) {
+      // this lane hashes rows [8*odd, 8*odd + 8) for the key pair (key & ~1, key | 1)
+      uint32_t hv[8];
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        st = mfma32(rd_row(Ki, kb * 32 + (lane & 31), 2 * s + hh), qf[s], st);
-        dp = mfma32(rd_row(Vi, kb * 32 + (lane & 31), 2 * s + hh), of[s], dp);
+      for (int i = 0; i < 8; ++i) {
+        const int r = 8 * odd + i;
+        const int qr = qb * 32 + acc_row(r, hh);
+        hv[i] = fer_hash(seed, (((uint64_t)bh * N + qr) * (uint64_t)NP + (key & ~1)) >> 1);
       }
+      keep = 0;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int key = kb * 32 + acc_row(r, hh);
-        const float p = key < N ? exp2f(st[r] * sl2 - lq) : 0.f;
-        float g = dp[r];
-        if (thr) g = drop_keep(seed, rowidx + key, thr) ? g * dscale : 0.f;
-        st[r] = p * (g - dq);
-      }
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        const bf16x8 df = pack8(st, s2);
-#pragma unroll
-        for (int db = 0; db < 2; ++db) dqt[db] = mfma32(rd_tr(Ki, kb * 32 + 16 * s2, db * 32, lane), df, dqt[db]);
+      for (int i = 0; i < 8; ++i) {
+        const uint32_t other = (uint32_t)__shfl_xor((int)hv[i], 1, 64);
+        const uint32_t h_lo = odd ? other : hv[i];  // rows i (even lane's own)
+        const uint32_t h_hi = odd ? hv[i] : other;  // rows 8 + i
+        const uint32_t u_lo = odd ? (h_lo >> 16) : (h_lo & 0xFFFFu);
+        const uint32_t u_hi = odd ? (h_hi >> 16) : (h_hi & 0xFFFFu);
+        keep |= (uint32_t)(u_lo >= thr) << i;
+        keep |= (uint32_t)(u_hi >= thr) << (8 + i);
       }
     }
-    if (q < N) {
-      bf16* o = dqkv + ((long)b * N + q) * lddq + h * dh;
+    f32x16 pd;
 #pragma unroll
-      for (int db = 0; db < 2; ++db)
+    for (int r = 0; r < 16; ++r) {
+      const int qr = qb * 32 + acc_row(r, hh);
+      const float p = kval ? exp2f(st[r] * sl2 - lse_s[qr]) : 0.f;
+      const bool kp = (keep >> r) & 1;
+      const float g = thr ? (kp ? dp[r] * dscale : 0.f) : dp[r];
+      pd[r] = thr ? (kp ? p * dscale : 0.f) : p;
+      st[r] = p * (g - dd_s[qr]);
+    }
 #pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) {
-          const int d = db * 32 + 8 * g4 + 4 * hh;
-          if (d < dh)
-            *(bf16x4*)(o + d) = bf16x4{(bf16)(dqt[db][4 * g4] * scale), (bf16)(dqt[db][4 * g4 + 1] * scale),
-                                       (bf16)(dqt[db][4 * g4 + 2] * scale), (bf16)(dqt[db][4 * g4 + 3] * scale)};
-        }
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const bf16x8 pf = pack8(pd, s2), df = pack8(st, s2);
+#pragma unroll
+      for (int db = 0; db < 2; ++db) {
+        dv[db] = mfma32(pf, rd_tr(Oi, qb * 32 + 16 * s2, db * 32, lane), dv[db]);
+        dk[db] = mfma32(df, rd_tr(Qi, qb * 32 + 16 * s2, db * 32, lane), dk[db]);
+      }
     }
   }
-  // ---------------- phase 2: wave w owns key block w -> dK, dV
-  {
-    const int key = w * 32 + (lane & 31);
-    bf16x8 kf[4], vf[4];
+  // dk/dv[db][r]: key row = w*32 + acc_row(r, hh), d = db*32 + (lane&31). Stage each wave's
+  // 32 x 64 tiles through LDS (rows of 128 B, no reuse across waves) for 16-byte row stores.
+  __syncthreads();
+  bf16* stg = (bf16*)(lds + w * 8192);  // [2][32][64]
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      kf[s] = rd_row(Ki, key, 2 * s + hh);
-      vf[s] = rd_row(Vi, key, 2 * s + hh);
+  for (int db = 0; db < 2; ++db)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int kr = acc_row(r, hh), d = db * 32 + (lane & 31);
+      stg[kr * 64 + d] = (bf16)(dk[db][r] * scale);
+      stg[2048 + kr * 64 + d] = (bf16)dv[db][r];
     }
-    f32x16 dk[2] = {f32x16{}, f32x16{}}, dv[2] = {f32x16{}, f32x16{}};
-    const bool kval = key < N;
-    for (int qb = 0; qb < NB; ++qb) {
-      f32x16 st = {}, dp = {};
+  // (wave-private region: LDS accesses of one wave complete in order)
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        st = mfma32(rd_row(Qi, qb * 32 + (lane & 31), 2 * s + hh), kf[s], st);
-        dp = mfma32(rd_row(Oi, qb * 32 + (lane & 31), 2 * s + hh), vf[s], dp);
-      }
-      f32x16 pd;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int q = qb * 32 + acc_row(r, hh);
-        const float p = kval ? exp2f(st[r] * sl2 - lse_s[q]) : 0.f;
-        float g = dp[r], pdv = p;
-        if (thr) {
-          const bool keep = drop_keep(seed, ((uint64_t)bh * N + q) * (uint64_t)N + key, thr);
-          g = keep ? g * dscale : 0.f;
-          pdv = keep ? p * dscale : 0.f;
-        }
-        pd[r] = pdv;
-        st[r] = p * (g - dd_s[q]);
-      }
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        const bf16x8 pf = pack8(pd, s2), df = pack8(st, s2);
-#pragma unroll
-        for (int db = 0; db < 2; ++db) {
-          dv[db] = mfma32(pf, rd_tr(Oi, qb * 32 + 16 * s2, db * 32, lane), dv[db]);
-          dk[db] = mfma32(df, rd_tr(Qi, qb * 32 + 16 * s2, db * 32, lane), dk[db]);
-        }
-      }
-    }
-    // dk/dv[db][r]: key row = w*32 + acc_row(r), d = db*32 + (lane&31)
-#pragma unroll
-    for (int db = 0; db < 2; ++db) {
-      const int d = db * 32 + (lane & 31);
-      if (d >= dh) continue;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int kr = w * 32 + acc_row(r, hh);
-        if (kr < N) {
-          bf16* o = dqkv + ((long)b * N + kr) * lddq;
-          o[D + h * dh + d] = (bf16)(dk[db][r] * scale);
-          o[2 * D + h * dh + d] = (bf16)dv[db][r];
-        }
-      }
-    }
+  for (int i = 0; i < 8; ++i) {
+    const int t = i * 64 + lane;          // 512 chunks of 16 B: [2 mats][32 rows][8 chunks]
+    const int mat = t >> 8, kr = (t >> 3) & 31, c = t & 7;
+    const int gk = w * 32 + kr;
+    if (gk < N && c * 8 < dh)
+      *(bf16x8*)(dqkv + ((long)b * N + gk) * lddq + (1 + mat) * D + h * dh + c * 8) =
+          *(const bf16x8*)(stg + mat * 2048 + kr * 64 + c * 8);
   }
 }
 
@@ -329,7 +412,7 @@ __global__ void attn_f32_pv(const float* P, const float* qkv, long ldq, float* o
   if (idx >= total) return;
   const int d = idx % dh, q = (idx / dh) % N, bh = idx / ((long)dh * N), b = bh / H, h = bh % H, D = H * dh;
   const float* pr = P + ((long)bh * N + q) * N;
-  const uint64_t rowidx = ((uint64_t)bh * N + q) * (uint64_t)N;
+  const uint64_t rowidx = drop_row(bh, N, q);
   float s = 0.f;
   for (int k = 0; k < N; ++k) {
     float p = pr[k];
@@ -354,7 +437,7 @@ __global__ void attn_f32_ds(const float* P, float* G, const float* qkv, long ldq
     const float* v = qkv + ((long)b * N + k) * ldq + 2 * D + h * dh;
     float dp = 0.f;
     for (int d = 0; d < dh; ++d) dp = fmaf(g[d], v[d], dp);
-    if (thr) dp = drop_keep(seed, (uint64_t)r * N + k, thr) ? dp * dscale : 0.f;
+    if (thr) dp = drop_keep(seed, drop_row(bh, N, q) + k, thr) ? dp * dscale : 0.f;
     G[r * N + k] = P[r * N + k] * (dp - dd);
   }
 }
@@ -371,7 +454,7 @@ __global__ void attn_f32_grads(const float* P, const float* G, const float* qkv,
     dq = fmaf(G[(rb + t) * N + j], qkv[((long)b * N + j) * ldq + D + h * dh + d], dq);
     dk = fmaf(G[(rb + j) * N + t], qkv[((long)b * N + j) * ldq + h * dh + d], dk);
     float p = P[(rb + j) * N + t];
-    if (thr) p = drop_keep(seed, (uint64_t)(rb + j) * N + t, thr) ? p * dscale : 0.f;
+    if (thr) p = drop_keep(seed, drop_row(bh, N, j) + t, thr) ? p * dscale : 0.f;
     dv = fmaf(p, dout[((long)b * N + j) * lddo + h * dh + d], dv);
   }
   float* o = dqkv + ((long)b * N + t) * lddq + h * dh + d;
@@ -417,6 +500,7 @@ extern "C" int fer_attention_fwd(int dtype, const void* qkv, int64_t ld_qkv, voi
   }
   if (N > 256 || dh > 64 || dh % 8) return set_error("attention_fwd(bf16): needs N <= 256, dh <= 64, dh % 8 == 0");
   if (ld_qkv % 8 || ld_out % 4) return set_error("attention_fwd(bf16): misaligned leading dimension");
+  if ((long)B * N * ld_qkv * 2 >= 0x7FFFFFF0L) return set_error("attention_fwd(bf16): qkv exceeds 2 GiB");
   const int nb = (N + 31) / 32;
   const float sl2 = scale * LOG2E;
   FER_NB_SWITCH(nb, hipLaunchKernelGGL(attn_fwd_bf16<NB_>, dim3(B * H), dim3(64 * NB_), 0, st, (const bf16*)qkv,
@@ -448,12 +532,18 @@ extern "C" int fer_attention_bwd(int dtype, const void* qkv, int64_t ld_qkv, con
     return hip_check("attention_bwd_f32");
   }
   if (N > 256 || dh > 64 || dh % 8) return set_error("attention_bwd(bf16): needs N <= 256, dh <= 64, dh % 8 == 0");
-  if (ld_qkv % 8 || ld_out % 8 || ld_dout % 8 || ld_dqkv % 4) return set_error("attention_bwd(bf16): misaligned ld");
+  if (ld_qkv % 8 || ld_out % 8 || ld_dout % 8 || ld_dqkv % 8) return set_error("attention_bwd(bf16): misaligned ld");
+  if ((long)B * N * ld_qkv * 2 >= 0x7FFFFFF0L || (long)B * N * ld_dout * 2 >= 0x7FFFFFF0L)
+    return set_error("attention_bwd(bf16): operand exceeds 2 GiB (buffer-resource range)");
   const int nb = (N + 31) / 32;
   const float sl2 = scale * LOG2E;
-  FER_NB_SWITCH(nb, hipLaunchKernelGGL(attn_bwd_bf16<NB_>, dim3(B * H), dim3(64 * NB_), 0, st, (const bf16*)qkv,
+  FER_NB_SWITCH(nb, hipLaunchKernelGGL(attn_dq_bf16<NB_>, dim3(B * H), dim3(64 * NB_), 0, st, (const bf16*)qkv,
                                        (long)ld_qkv, (const bf16*)out, (long)ld_out, (const bf16*)dout, (long)ld_dout,
                                        lse, (bf16*)dqkv, (long)ld_dqkv, N, H, dh, scale, sl2, drop_thresh, drop_scale,
-                                       seed));
+                                       seed);
+                hipLaunchKernelGGL(attn_dkv_bf16<NB_>, dim3(B * H), dim3(64 * NB_), 0, st, (const bf16*)qkv,
+                                   (long)ld_qkv, (const bf16*)out, (long)ld_out, (const bf16*)dout, (long)ld_dout,
+                                   lse, (bf16*)dqkv, (long)ld_dqkv, N, H, dh, scale, sl2, drop_thresh, drop_scale,
+                                   seed));
   return hip_check("attention_bwd_bf16");
 }

@@ -190,7 +190,8 @@ def test_attention_fwd_bwd(N, H, dh, dtype, p):
     out = torch.empty(B * N, D, device=DEV, dtype=qd.dtype)
     lse = torch.empty(B * H * N, device=DEV)
     o.attention_fwd(qd, out, lse, B, N, H, dh, dropout=p, seed=seed)
-    keep = keep_mask(seed, (B, H, N, N), p) if p > 0 else None
+    # attention dropout index: (bh*N + q)*NP + k, NP = N rounded up to even (csrc/attention.hip)
+    keep = keep_mask(seed, (B, H, N, N + (N & 1)), p)[..., :N] if p > 0 else None
     qr = qd.float().cpu().requires_grad_(True)
     ref, lse_ref = attn_ref(qr, B, N, H, dh, keep, p)
     assert rel_err(out.cpu(), ref) < tol
