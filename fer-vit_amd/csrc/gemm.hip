@@ -31,6 +31,74 @@
 namespace fer {
 
 // ------------------------------------------------------------------- epilogue
+// bf16 tile epilogue on 8 consecutive columns (one 16-byte store per output row piece; the
+// store issue rate, not bandwidth, bounds a tile's store tail). x = res[m][n..n+7] when e.res
+// is set, else aux[m][n..n+7] (only when both are set is aux loaded here, a path no caller of
+// the hot path takes). b0/b1 = bias of the 8 columns, ps = *post_scale, both loaded once.
+FER_DEV f32x4 lo4(bf16x8 x) { return f32x4{(float)x[0], (float)x[1], (float)x[2], (float)x[3]}; }
+FER_DEV f32x4 hi4(bf16x8 x) { return f32x4{(float)x[4], (float)x[5], (float)x[6], (float)x[7]}; }
+FER_DEV bf16x8 pack8(f32x4 a, f32x4 b) {
+  return bf16x8{(bf16)a[0], (bf16)a[1], (bf16)a[2], (bf16)a[3], (bf16)b[0], (bf16)b[1], (bf16)b[2], (bf16)b[3]};
+}
+FER_DEV void epi8_bf16(const EpiArgs& e, long m, long n, f32x4 v0, f32x4 v1, f32x4 b0, f32x4 b1, bf16x8 x,
+                       float ps) {
+  v0 = v0 * e.alpha + b0;
+  v1 = v1 * e.alpha + b1;
+  if (e.pre) *(bf16x8*)((bf16*)e.pre + m * e.ldp + n) = pack8(v0, v1);
+  if (e.act == FER_ACT_GELU) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      v0[r] = gelu_erf(v0[r]);
+      v1[r] = gelu_erf(v1[r]);
+    }
+  } else if (e.act == FER_ACT_RELU) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      v0[r] = fmaxf(v0[r], 0.f);
+      v1[r] = fmaxf(v1[r], 0.f);
+    }
+  }
+  if (e.drop_thresh) {
+    const uint64_t idx = (uint64_t)m * (uint64_t)e.drop_ld + (uint64_t)n;
+    drop4(e.seed, idx, e.drop_thresh, e.drop_scale, v0);
+    drop4(e.seed, idx + 4, e.drop_thresh, e.drop_scale, v1);
+  }
+  if (e.post_scale) {
+    v0 *= ps;
+    v1 *= ps;
+  }
+  if (e.aux) {
+    const bf16x8 a = e.res ? *(const bf16x8*)((const bf16*)e.aux + m * e.ldx + n) : x;
+    const f32x4 a0 = lo4(a), a1 = hi4(a);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      v0[r] *= act_grad(e.aux_act, a0[r]);
+      v1[r] *= act_grad(e.aux_act, a1[r]);
+    }
+  }
+  if (e.res) {
+    v0 += lo4(x);
+    v1 += hi4(x);
+  }
+  if (e.c_f32) {
+    float* c = (float*)e.c + m * e.ldc + n;
+    if (e.accumulate) {
+      v0 += *(const f32x4*)c;
+      v1 += *(const f32x4*)(c + 4);
+    }
+    *(f32x4*)c = v0;
+    *(f32x4*)(c + 4) = v1;
+  } else {
+    bf16* c = (bf16*)e.c + m * e.ldc + n;
+    if (e.accumulate) {
+      const bf16x8 o = *(const bf16x8*)c;
+      v0 += lo4(o);
+      v1 += hi4(o);
+    }
+    *(bf16x8*)c = pack8(v0, v1);
+  }
+}
+
 template <typename T>
 FER_DEV void epi4(const EpiArgs& e, long m, long n, f32x4 v) {
   v *= e.alpha;
@@ -195,7 +263,7 @@ FER_DEV typename Acc<MT>::T mfma(bf16x8 a, bf16x8 b, typename Acc<MT>::T c) {
 // the fp32 slab; otherwise each wave-row half of the tile (in EPC row chunks) is staged
 // through LDS as fp32 with padded rows and every thread applies the epilogue on 4 consecutive
 // columns of one row: all global traffic of the epilogue is row-contiguous.
-template <int BM, int BN, int WM, int WN, int MT, int EPC, typename AccT, int FN, int FM>
+template <int BM, int BN, int WM, int WN, int MT, int EPC, int SMEMB, typename AccT, int FN, int FM>
 FER_DEV void tile_epilogue(const GemmArgs& g, const EpiArgs& e, AccT (&acc)[FN][FM], char* smem, int m0, int n0,
                            int ks, int wm, int wn, int lane) {
   constexpr int TM = BM / WM, TN = BN / WN;
@@ -218,34 +286,111 @@ FER_DEV void tile_epilogue(const GemmArgs& g, const EpiArgs& e, AccT (&acc)[FN][
     return;
   }
   static_assert(WM == 2, "epilogue staging splits the tile by the wave-row halves");
-  constexpr int EROWS = TM / EPC, ELD = BN + 4, FJ = FM / EPC;
+  static_assert(EPC == 1 || EPC == 2, "chunk pairing assumes 1 or 2 chunks per wave-row half");
+  constexpr int EROWS = TM / EPC, FJ = FM / EPC;  // rows per chunk; MFMA row blocks per chunk
   static_assert(FJ * EPC == FM, "row chunks must split the MFMA blocks evenly");
-  float* ep = (float*)smem;
-  constexpr int NT = 64 * WM * WN;
-  constexpr int C4 = BN / 4;  // float4 groups per row
+  constexpr int NT = 64 * WM * WN, NW = WM * WN;
+  constexpr int C8 = BN / 8;                     // 8-column groups per row
+  static_assert(NT % C8 == 0, "each thread keeps one column group for the whole tile");
+  constexpr int RPI = NT / C8, IT = EROWS / RPI;  // rows per pass, passes per chunk
+  static_assert(IT * RPI == EROWS, "chunk rows must split evenly over the passes");
+  // LDS: [staging: EROWS x BN fp32, 16-byte chunks XOR-swizzled by (row & 7)]
+  //      [X0 | X1: EROWS x BN bf16 each, the chunk's residual / aux rows]
+  constexpr int SROW = BN * 4, XBYTES = EROWS * BN * 2;
+  constexpr int NP = XBYTES / 1024, PPW = NP / NW;     // 1 KB DMA pieces per chunk / per wave
+  constexpr int RPP = 1024 / (BN * 2), LPR = BN / 8;   // rows per piece, lanes per row
+  static_assert(PPW * NW == NP && RPP * LPR == 64, "X tile must split into whole 1 KB pieces per wave");
+  static_assert(EROWS * SROW + 2 * XBYTES <= SMEMB, "epilogue staging + X buffers exceed the kernel's LDS");
+  char* const stg = smem;
+  char* const xb = smem + EROWS * SROW;
+  auto swz = [](int row, int col) { return row * SROW + ((((col >> 2) ^ (row & 7))) << 4); };
+
+  // Each thread owns 4 consecutive columns for the whole tile (bias loaded once) and rows
+  // tr + RPI*it of every chunk. The residual / aux rows ("x") of chunk h+1 are brought into
+  // LDS by LDS-DMA while chunk h is processed. vmcnt retires loads, stores and DMA in issue
+  // order, so each DMA is issued BEFORE the previous chunk's stores... and waited for with a
+  // count that skips exactly those stores; the item loop itself never waits on memory.
+  const int tc = (threadIdx.x % C8) * 8, tr = threadIdx.x / C8;
+  const int wave = threadIdx.x >> 6;
+  const long n = n0 + tc;
+  const bool nok = n < g.N;  // N % 8 == 0 on this path (checked by the host)
+  f32x4 b0 = f32x4{0.f, 0.f, 0.f, 0.f}, b1 = b0;
+  if (e.bias && nok) {
+    b0 = *(const f32x4*)(e.bias + n);
+    b1 = *(const f32x4*)(e.bias + n + 4);
+  }
+  const float ps = e.post_scale ? *e.post_scale : 1.f;
+  const void* xs = e.res ? e.res : e.aux;  // the row operand brought in by DMA
+  const long ldxs = e.res ? e.ldr : e.ldx;
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(xs);
+  // this lane's DMA source for piece k of chunk 0 (rows advance by EROWS per chunk)
+  const int xrow = lane / LPR, xcol = (lane % LPR) * 8;
+  const bool xcol_ok = n0 + xcol + 8 <= g.N;
+  auto issue_x = [&](int h) {
+    char* dst = xb + (h & 1) * XBYTES;
 #pragma unroll
-  for (int h = 0; h < 2 * EPC; ++h) {
-    __syncthreads();
-    if (wm == h / EPC) {
+    for (int k = 0; k < PPW; ++k) {
+      const int piece = wave * PPW + k;
+      const long m = m0 + h * EROWS + piece * RPP + xrow;
+      const uint32_t voff = (xcol_ok && m < g.M) ? (uint32_t)((m * ldxs + n0 + xcol) * 2) : FER_OOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_void*)(dst + piece * 1024), 16, voff, 0, 0, 0);
+    }
+  };
+  // Stores per wave per chunk when every row of the tile is in range (else a full drain).
+  const bool full = m0 + BM <= g.M && !e.accumulate && !(e.res && e.aux);
+  const int spc = full ? IT * (e.pre ? 2 : 1) : -1;
+  auto wait_x = [&](int pending) {  // wait until the DMA of the current chunk has landed
+    switch (pending) {
+      case 0: wait_vm<0>(); break;
+      case 4: wait_vm<4>(); break;
+      case 8: wait_vm<8>(); break;
+      case 12: wait_vm<12>(); break;
+      case 16: wait_vm<16>(); break;
+      case 20: wait_vm<20>(); break;
+      default: wait_vm<0>(); break;
+    }
+  };
+  auto stage = [&](int h, int half, int sub) {
+    __syncthreads();  // every wave is done with the staging area and with X[(h+1)&1]
+    const bool more = h + 1 < 2 * EPC;
+    if (xs && more) issue_x(h + 1);
+    if (wm == half) {
 #pragma unroll
       for (int i = 0; i < FN; ++i)
 #pragma unroll
         for (int jj = 0; jj < FJ; ++jj)
 #pragma unroll
           for (int q = 0; q < NQ; ++q) {
-            const int j = (h % EPC) * FJ + jj;
-            const int r = jj * MT + lr;
-            const int c = wn * TN + i * MT + 8 * q + lc;
-            *(f32x4*)(ep + r * ELD + c) =
+            const int j = sub * FJ + jj;
+            *(f32x4*)(stg + swz(jj * MT + lr, wn * TN + i * MT + 8 * q + lc)) =
                 f32x4{acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]};
           }
     }
-    __syncthreads();
-    for (int idx = threadIdx.x; idx < EROWS * C4; idx += NT) {
-      const int r = idx / C4, c = (idx - r * C4) * 4;
-      const long m = m0 + h * EROWS + r, n = n0 + c;
-      if (m < g.M && n < g.N) epi4<bf16>(e, m, n, *(const f32x4*)(ep + r * ELD + c));
+    if (xs) {
+      const int after = (more ? PPW : 0) + (h > 0 ? spc : 0);
+      wait_x(spc < 0 ? 0 : after);
     }
+    __syncthreads();  // staging and X[h&1] (all waves' DMA) visible
+  };
+  auto finish = [&](int h) {
+    const char* xh = xb + (h & 1) * XBYTES;
+#pragma unroll 1
+    for (int it = 0; it < IT; ++it) {
+      const int r = tr + it * RPI;
+      const long m = m0 + h * EROWS + r;
+      const f32x4 v0 = *(const f32x4*)(stg + swz(r, tc)), v1 = *(const f32x4*)(stg + swz(r, tc + 4));
+      const bf16x8 x = xs ? *(const bf16x8*)(xh + (r * BN + tc) * 2) : bf16x8{};
+      if (nok && m < g.M) epi8_bf16(e, m, n, v0, v1, b0, b1, x, ps);
+    }
+  };
+  if (xs) issue_x(0);
+#pragma unroll 1
+  for (int p = 0; p < EPC; ++p) {
+    const int h0 = 2 * p, h1 = 2 * p + 1;
+    stage(h0, h0 / EPC, 0);
+    finish(h0);
+    stage(h1, h1 / EPC, EPC == 2 ? 1 : 0);
+    finish(h1);
   }
 }
 
@@ -352,7 +497,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g, 
     if (acc[0][0][0] == 12345.f) g.ws[0] = 1.f;  // keep the MFMAs alive
     return;
   }
-  tile_epilogue<BM, BN, WM, WN, MT, 1>(g, e, acc, smem, m0, n0, ks, wm, wn, lane);
+  tile_epilogue<BM, BN, WM, WN, MT, (BM >= 256 ? 2 : 1), SMEM>(g, e, acc, smem, m0, n0, ks, wm, wn, lane);
 }
 
 // Ring variant: BK=32 stages in an NST-slot LDS ring, LDS-DMA issued NST-1 K-steps ahead and
@@ -477,7 +622,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_ring_kernel(GemmArgs g, 
       for (int j = 0; j < FM; ++j) af[j] = an[j];
     }
   }
-  tile_epilogue<BM, BN, WM, WN, MT, EPC>(g, e, acc, smem, m0, n0, ks, wm, wn, lane);
+  tile_epilogue<BM, BN, WM, WN, MT, EPC, NST * STAGE>(g, e, acc, smem, m0, n0, ks, wm, wn, lane);
 }
 
 // ===================================================================== 8-phase kernel
@@ -646,7 +791,7 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmArgs g, EpiArgs e)
   }
   if (nk > 0 && !wr) __builtin_amdgcn_s_barrier();  // waves 0-3 catch up with the stagger
   static_assert(64 * (256 + 4) * 4 <= 2 * BUF, "epilogue staging (2 chunks per half) must fit");
-  tile_epilogue<256, 256, 2, 4, MT, 2>(g, e, acc, smem, m0, n0, ks, wr, wc, lane);
+  tile_epilogue<256, 256, 2, 4, MT, 2, 2 * BUF>(g, e, acc, smem, m0, n0, ks, wr, wc, lane);
 }
 
 // Ordered (deterministic) split-K reduction + epilogue.
@@ -784,6 +929,12 @@ int gemm_launch(const GemmDesc& d, const EpiArgs& e_in, hipStream_t st) {
     return set_error("gemm: A layout needs 8-element aligned rows");
   if ((d.b_kc && (d.K % 8 || d.ldb % 8)) || (!d.b_kc && (d.N % 8 || d.ldb % 8)))
     return set_error("gemm: B layout needs 8-element aligned rows");
+  // epilogue row operand (res / aux) is fetched by 16-byte LDS-DMA pieces
+  // The tile epilogue works on 16-byte row pieces (8 bf16): output, pre-activation and the
+  // res / aux operand (fetched by LDS-DMA) need 8-element aligned rows.
+  auto al8 = [](const void* p, long ld) { return !p || (ld % 8 == 0 && (uintptr_t)p % 16 == 0); };
+  if (d.N % 8 || !al8(e.c, e.ldc) || !al8(e.pre, e.ldp) || !al8(e.res, e.ldr) || !al8(e.aux, e.ldx))
+    return set_error("gemm: bf16 path needs N and every epilogue row stride multiples of 8 (16-byte aligned rows)");
   const long a_bytes = (d.a_kc ? (long)(d.M - 1) * d.lda + d.K : (long)(d.K - 1) * d.lda + d.M) * 2;
   const long b_bytes = (d.b_kc ? (long)(d.N - 1) * d.ldb + d.K : (long)(d.K - 1) * d.ldb + d.N) * 2;
   if (a_bytes >= 0x7FFFFFF0L || b_bytes >= 0x7FFFFFF0L) return set_error("gemm: operand exceeds 2 GiB");
