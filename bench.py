@@ -97,6 +97,51 @@ class GemmProbe:
         return sum(ts) / max(1, len(ts)), len(ts)
 
 
+def pmc_traffic(timeout_s=120):
+    """HBM bytes per launch of the roofline kernel from rocprofv3 PMC counters, one counter per
+    pass (MI355X_MICROARCH.md: FETCH_SIZE / WRITE_SIZE in KiB; on gfx950 FETCH_SIZE reads half the
+    bytes of a 16 B/lane streaming read -- the GEMM's LDS-DMA operand loads -- so it is doubled;
+    WRITE_SIZE is exact for 16 B/lane stores). Runs tools/traffic_probe.py as a CHILD process under
+    rocprofv3 before this process touches the GPU. Returns (bytes, detail) or (None, reason)."""
+    import csv
+    import glob
+    import shutil
+    import subprocess
+    import tempfile
+
+    exe = shutil.which("rocprofv3")
+    if exe is None:
+        return None, "rocprofv3 not found"
+    probe = os.path.join(ROOT, "tools", "traffic_probe.py")
+    vals = {}
+    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = tempfile.mkdtemp(prefix=f"pmc_{ctr}_", dir=os.environ.get("TMPDIR", "/tmp"))
+        cmd = ["timeout", "-s", "KILL", str(timeout_s), exe, "--pmc", ctr, "--output-format", "csv", "-d", d,
+               "-o", "p", "--", sys.executable, probe]
+        try:
+            r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, timeout=timeout_s + 30)
+        except Exception as ex:  # noqa: BLE001
+            return None, f"{ctr} pass failed: {ex}"
+        files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+        if r.returncode != 0 or not files:
+            return None, f"{ctr} pass rc={r.returncode}: {r.stdout.decode(errors='replace')[-300:]}"
+        per = []
+        with open(files[0]) as f:
+            for row in csv.DictReader(f):
+                if "gemm" in row.get("Kernel_Name", "") and row.get("Counter_Name", "") == ctr:
+                    per.append(float(row["Counter_Value"]))
+        shutil.rmtree(d, ignore_errors=True)
+        if not per:
+            return None, f"{ctr}: no gemm dispatch in the counter CSV"
+        per.sort()
+        vals[ctr] = per[len(per) // 2]  # median over the probe's launches (KiB)
+    read_b = 2.0 * vals["FETCH_SIZE"] * 1024
+    write_b = vals["WRITE_SIZE"] * 1024
+    return read_b + write_b, {"read_bytes": read_b, "write_bytes": write_b, "fetch_size_kib": vals["FETCH_SIZE"],
+                              "write_size_kib": vals["WRITE_SIZE"], "method": "rocprofv3 --pmc, one counter per "
+                              "pass, median over 6 launches; read = 2*FETCH_SIZE (gfx950 16 B/lane correction)"}
+
+
 def cpu_baseline(cfg_name, budget_s=20.0):
     """Oracle train step (fp32, torch CPU ops) on a bounded sample of the workload."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -171,11 +216,16 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="vit_base_224", choices=list(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC traffic passes")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    traffic, traffic_detail = None, "not measured (N>1 or --no-traffic)"
+    if world == 1 and not args.no_traffic and args.config == "vit_base_224":
+        # child rocprofv3 passes first: this process has not initialised the GPU yet
+        traffic, traffic_detail = pmc_traffic()
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
     if world > 1:
@@ -237,6 +287,8 @@ def main():
     imgs = world * B * args.steps / el
     step_tflops = flops_img * B / (ms / 1e3) / 1e12
     gemm_flop = 2.0 * B * N * F * D
+    # bytes the fc1 launch must move at minimum: X [BN x D] + W1 [F x D] read, pre + out [BN x F] written (bf16)
+    algo_bytes = 2 * (B * N * D + F * D + 2 * B * N * F)
     achieved = gemm_flop / (gemm_ms / 1e3) / 1e12
     lossv = loss.item()
     if rank == 0:
@@ -251,7 +303,10 @@ def main():
                        "parallelism": f"dp{world}"},
             "roofline": {"bound": "mfma", "kernel": f"gemm_bf16 linear1 fwd [{B * N}x{D}]x[{F}x{D}]^T",
                          "achieved": round(achieved, 1), "peak": round(PEAK_BF16_TFLOPS, 1), "unit": "TFLOP/s",
-                         "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None,
+                         "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
+                         "traffic": None if traffic is None else round(traffic),
+                         "traffic_detail": traffic_detail,
+                         "algorithmic_bytes": algo_bytes,
                          "launches_timed": nlaunch, "mean_launch_ms": round(gemm_ms, 4)},
             "step_mfma_frac": round(step_tflops / PEAK_BF16_TFLOPS, 4),
             "step_tflops": round(step_tflops, 1),

@@ -15,7 +15,7 @@ timeout -k 10 300 python -u bench.py --steps $STEPS --warmup 5 > gpurun_out/benc
   || { tail -20 gpurun_out/bench_$TAG.txt; exit 1; }
 tail -1 gpurun_out/bench_$TAG.txt
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o run \
-  -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/prof_$TAG.log 2>&1 \
+  -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-traffic > gpurun_out/prof_$TAG.log 2>&1 \
   || { tail -20 gpurun_out/prof_$TAG.log; exit 1; }
 tail -1 gpurun_out/prof_$TAG.log
 f=$(find gpurun_out/prof_$TAG -name '*kernel_stats.csv' | head -1)
