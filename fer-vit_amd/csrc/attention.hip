@@ -72,19 +72,23 @@ FER_DEV int acc_row(int reg, int hh) { return (reg & 3) + 8 * (reg >> 2) + 4 * h
 
 // Dropout element index of P[bh][q][k]: (bh*N + q)*NP + k with NP = N rounded up to even, so
 // keys 2j, 2j+1 of one query share one 32-bit hash (one 16-bit half each).
-FER_DEV uint64_t drop_row(int bh, int N, int q) { return ((uint64_t)bh * N + q) * (uint64_t)(N + (N & 1)); }
+FER_DEV uint32_t drop_row(int bh, int N, int q) { return ((uint32_t)bh * N + q) * (uint32_t)(N + (N & 1)); }
 
-// Keep flags of the 16 accumulator registers when registers hold KEYS (S^T orientation:
-// registers 2i, 2i+1 are consecutive keys, first one even): 8 hashes per lane.
-FER_DEV uint32_t keep16_keys(uint64_t seed, uint64_t row, int kb, int hh, uint32_t thr) {
-  uint32_t bits = 0;
+// v_exp_f32 without the denormal range fix-up of exp2f: arguments here are <= 0 (scores minus
+// the running max / the logsumexp), results below 2^-126 flush to 0 and -inf gives 0.
+FER_DEV float ex2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// Dropout of the 16 accumulator registers when registers hold KEYS (S^T orientation): registers
+// 2i, 2i+1 are consecutive keys (the first even) = the two halves of one hash. v[r] *= keep ?
+// dscale : 0 for every register.
+FER_DEV void drop16_keys(uint64_t seed, uint32_t row, int kb, int hh, uint32_t thr, float dscale, f32x16& v) {
+  const uint32_t p0 = (row >> 1) + kb * 16 + 2 * hh;  // pair of register 0
 #pragma unroll
   for (int r = 0; r < 16; r += 2) {
-    const uint32_t h = fer_hash(seed, (row + kb * 32 + acc_row(r, hh)) >> 1);
-    bits |= (uint32_t)((h & 0xFFFFu) >= thr) << r;
-    bits |= (uint32_t)((h >> 16) >= thr) << (r + 1);
+    const uint32_t h = fer_hash(seed, p0 + (uint32_t)(acc_row(r, 0) >> 1));
+    v[r] = (h & 0xFFFFu) >= thr ? v[r] * dscale : 0.f;
+    v[r + 1] = (h >> 16) >= thr ? v[r + 1] * dscale : 0.f;
   }
-  return bits;
 }
 
 // rows [0, 32*NB) of a [N][dh] column block -> swizzled LDS image by LDS-DMA (16 B per lane,
@@ -142,7 +146,7 @@ __global__ __launch_bounds__(64 * NB) __attribute__((amdgpu_waves_per_eu(4))) vo
   }
   __syncthreads();  // vmcnt(0) + barrier: every wave's DMA pieces have landed
 
-  const uint64_t row = drop_row(bh, N, q);
+  const uint32_t row = drop_row(bh, N, q);
   float m = -INFINITY, l = 0.f;
   f32x16 ot[2] = {f32x16{}, f32x16{}};
 #pragma unroll 1
@@ -150,27 +154,27 @@ __global__ __launch_bounds__(64 * NB) __attribute__((amdgpu_waves_per_eu(4))) vo
     f32x16 st = {};
 #pragma unroll
     for (int s = 0; s < 4; ++s) st = mfma32(rd_row(Ki, kb * 32 + (lane & 31), 2 * s + hh), qf[s], st);
-    float bm = -INFINITY;
+    if (kb * 32 + 32 > N) {  // only the last key block has padding keys (wave-uniform)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int key = kb * 32 + acc_row(r, hh);
-      st[r] = key < N ? st[r] * sl2 : -INFINITY;
-      bm = fmaxf(bm, st[r]);
+      for (int r = 0; r < 16; ++r)
+        if (kb * 32 + acc_row(r, hh) >= N) st[r] = -INFINITY;
     }
-    bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
+    float bm = st[0];
+#pragma unroll
+    for (int r = 1; r < 16; ++r) bm = fmaxf(bm, st[r]);
+    bm = fmaxf(bm, __shfl_xor(bm, 32, 64)) * sl2;
     const float mn = fmaxf(m, bm);
-    const float al = exp2f(m - mn);
+    const float al = ex2(m - mn);
     m = mn;
     l *= al;
 #pragma unroll
     for (int db = 0; db < 2; ++db) ot[db] *= al;
-    const uint32_t keep = thr ? keep16_keys(seed, row, kb, hh, thr) : 0xFFFFu;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const float e = exp2f(st[r] - mn);
-      l += e;
-      st[r] = thr ? ((keep >> r) & 1 ? e * dscale : 0.f) : e;
+      st[r] = ex2(fmaf(st[r], sl2, -mn));
+      l += st[r];
     }
+    if (thr) drop16_keys(seed, row, kb, hh, thr, dscale, st);
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
       const bf16x8 pf = pack8(st, s2);
@@ -222,7 +226,7 @@ __global__ __launch_bounds__(64 * NB) __attribute__((amdgpu_waves_per_eu(4))) vo
   const float lq = qv ? lse[(long)bh * N + q] * LOG2E : INFINITY;
   __syncthreads();
 
-  const uint64_t row = drop_row(bh, N, q);
+  const uint32_t row = drop_row(bh, N, q);
   f32x16 dqt[2] = {f32x16{}, f32x16{}};
 #pragma unroll 1
   for (int kb = 0; kb < NB; ++kb) {
@@ -232,13 +236,13 @@ __global__ __launch_bounds__(64 * NB) __attribute__((amdgpu_waves_per_eu(4))) vo
       st = mfma32(rd_row(Ki, kb * 32 + (lane & 31), 2 * s + hh), qf[s], st);
       dp = mfma32(rd_row(Vi, kb * 32 + (lane & 31), 2 * s + hh), of[s], dp);
     }
-    const uint32_t keep = thr ? keep16_keys(seed, row, kb, hh, thr) : 0xFFFFu;
+    if (thr) drop16_keys(seed, row, kb, hh, thr, dscale, dp);
+    const bool tail = kb * 32 + 32 > N;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int key = kb * 32 + acc_row(r, hh);
-      const float p = key < N ? exp2f(st[r] * sl2 - lq) : 0.f;
-      const float g = thr ? ((keep >> r) & 1 ? dp[r] * dscale : 0.f) : dp[r];
-      st[r] = p * (g - dsum);
+      float p = ex2(fmaf(st[r], sl2, -lq));
+      if (tail && kb * 32 + acc_row(r, hh) >= N) p = 0.f;
+      st[r] = p * (dp[r] - dsum);
     }
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
@@ -323,7 +327,7 @@ __global__ __launch_bounds__(64 * NB) void attn_dkv_bf16(const bf16* __restrict_
       for (int i = 0; i < 8; ++i) {
         const int r = 8 * odd + i;
         const int qr = qb * 32 + acc_row(r, hh);
-        hv[i] = fer_hash(seed, (((uint64_t)bh * N + qr) * (uint64_t)NP + (key & ~1)) >> 1);
+        hv[i] = fer_hash(seed, (((uint32_t)bh * N + qr) * (uint32_t)NP + (uint32_t)(key & ~1)) >> 1);
       }
       keep = 0;
 #pragma unroll
@@ -341,7 +345,7 @@ __global__ __launch_bounds__(64 * NB) void attn_dkv_bf16(const bf16* __restrict_
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int qr = qb * 32 + acc_row(r, hh);
-      const float p = kval ? exp2f(st[r] * sl2 - lse_s[qr]) : 0.f;
+      const float p = kval ? ex2(fmaf(st[r], sl2, -lse_s[qr])) : 0.f;
       const bool kp = (keep >> r) & 1;
       const float g = thr ? (kp ? dp[r] * dscale : 0.f) : dp[r];
       pd[r] = thr ? (kp ? p * dscale : 0.f) : p;
@@ -412,7 +416,7 @@ __global__ void attn_f32_pv(const float* P, const float* qkv, long ldq, float* o
   if (idx >= total) return;
   const int d = idx % dh, q = (idx / dh) % N, bh = idx / ((long)dh * N), b = bh / H, h = bh % H, D = H * dh;
   const float* pr = P + ((long)bh * N + q) * N;
-  const uint64_t rowidx = drop_row(bh, N, q);
+  const uint32_t rowidx = drop_row(bh, N, q);
   float s = 0.f;
   for (int k = 0; k < N; ++k) {
     float p = pr[k];
@@ -499,6 +503,8 @@ extern "C" int fer_attention_fwd(int dtype, const void* qkv, int64_t ld_qkv, voi
     return hip_check("attention_fwd_f32");
   }
   if (N > 256 || dh > 64 || dh % 8) return set_error("attention_fwd(bf16): needs N <= 256, dh <= 64, dh % 8 == 0");
+  if (check_drop_range(drop_thresh, (long)B * H * N * (N + (N & 1)), "attention_fwd: dropout over >= 2^32 probabilities"))
+    return -1;
   if (ld_qkv % 8 || ld_out % 4) return set_error("attention_fwd(bf16): misaligned leading dimension");
   if ((long)B * N * ld_qkv * 2 >= 0x7FFFFFF0L) return set_error("attention_fwd(bf16): qkv exceeds 2 GiB");
   const int nb = (N + 31) / 32;
@@ -532,6 +538,8 @@ extern "C" int fer_attention_bwd(int dtype, const void* qkv, int64_t ld_qkv, con
     return hip_check("attention_bwd_f32");
   }
   if (N > 256 || dh > 64 || dh % 8) return set_error("attention_bwd(bf16): needs N <= 256, dh <= 64, dh % 8 == 0");
+  if (check_drop_range(drop_thresh, (long)B * H * N * (N + (N & 1)), "attention_bwd: dropout over >= 2^32 probabilities"))
+    return -1;
   if (ld_qkv % 8 || ld_out % 8 || ld_dout % 8 || ld_dqkv % 8) return set_error("attention_bwd(bf16): misaligned ld");
   if ((long)B * N * ld_qkv * 2 >= 0x7FFFFFF0L || (long)B * N * ld_dout * 2 >= 0x7FFFFFF0L)
     return set_error("attention_bwd(bf16): operand exceeds 2 GiB (buffer-resource range)");

@@ -77,12 +77,14 @@ FER_DEV float act_grad(int act, float x) {
 
 // ---------------------------------------------------------------- dropout RNG
 // Counter-based and stateless: keep(seed, idx) is a pure function of the element's
-// linear index, so backward regenerates the forward mask. One 32-bit hash (lowbias32
-// finaliser) yields two 16-bit uniforms: element idx uses half (idx & 1) of
-// hash(seed, idx >> 1). Drop iff u16 < thresh, thresh = round(p * 65536).
-FER_DEV uint32_t fer_hash(uint64_t seed, uint64_t pair) {
-  uint32_t x = (uint32_t)pair * 0x9E3779B1u + (uint32_t)seed;
-  x ^= (uint32_t)(pair >> 32) * 0x85EBCA6Bu + (uint32_t)(seed >> 32);
+// linear index, so backward regenerates the forward mask. One 32-bit hash yields two 16-bit
+// uniforms: element idx uses half (idx & 1) of hash(seed, idx >> 1). Drop iff u16 < thresh,
+// thresh = round(p * 65536). The key enters by xor/add (a relabelling of the counter), the
+// lowbias32 finaliser does the mixing: 2 integer multiplies per pair of elements.
+// Element indices are 32-bit: every C-ABI entry point with dropout checks idx < 2^32
+// (fer::check_drop_range); index arithmetic is done mod 2^32 by the callers.
+FER_DEV uint32_t fer_hash(uint64_t seed, uint32_t pair) {
+  uint32_t x = (pair ^ (uint32_t)seed) + (uint32_t)(seed >> 32);
   x ^= x >> 16;
   x *= 0x7FEB352Du;
   x ^= x >> 15;
@@ -90,13 +92,13 @@ FER_DEV uint32_t fer_hash(uint64_t seed, uint64_t pair) {
   x ^= x >> 16;
   return x;
 }
-FER_DEV bool drop_keep(uint64_t seed, uint64_t idx, uint32_t thresh) {
+FER_DEV bool drop_keep(uint64_t seed, uint32_t idx, uint32_t thresh) {
   if (thresh == 0u) return true;
   const uint32_t h = fer_hash(seed, idx >> 1);
   return ((h >> ((idx & 1) * 16)) & 0xFFFFu) >= thresh;
 }
 // 4 consecutive elements starting at an even index: two hashes.
-FER_DEV void drop4(uint64_t seed, uint64_t idx, uint32_t thresh, float scale, f32x4& v) {
+FER_DEV void drop4(uint64_t seed, uint32_t idx, uint32_t thresh, float scale, f32x4& v) {
   if (thresh == 0u) return;
   const uint32_t h0 = fer_hash(seed, idx >> 1), h1 = fer_hash(seed, (idx >> 1) + 1);
   v[0] = (h0 & 0xFFFFu) >= thresh ? v[0] * scale : 0.f;

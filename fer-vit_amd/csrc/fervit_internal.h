@@ -32,4 +32,10 @@ void part_reduce(const float* part, int nb, long ld, int ncols, int seg, float* 
 
 inline int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
 
+// Dropout element indices are 32-bit (common.h fer_hash): a dropout site covers < 2^32 elements.
+inline int check_drop_range(uint32_t thresh, long elements, const char* what) {
+  if (thresh && elements > 0xFFFFFFFFL) return set_error(what);
+  return 0;
+}
+
 }  // namespace fer

@@ -59,7 +59,7 @@ FER_DEV void epi8_bf16(const EpiArgs& e, long m, long n, f32x4 v0, f32x4 v1, f32
     }
   }
   if (e.drop_thresh) {
-    const uint64_t idx = (uint64_t)m * (uint64_t)e.drop_ld + (uint64_t)n;
+    const uint32_t idx = (uint32_t)m * (uint32_t)e.drop_ld + (uint32_t)n;
     drop4(e.seed, idx, e.drop_thresh, e.drop_scale, v0);
     drop4(e.seed, idx + 4, e.drop_thresh, e.drop_scale, v1);
   }
@@ -108,7 +108,7 @@ FER_DEV void epi4(const EpiArgs& e, long m, long n, f32x4 v) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) v[r] = act_fwd(e.act, v[r]);
   }
-  if (e.drop_thresh) drop4(e.seed, (uint64_t)m * (uint64_t)e.drop_ld + (uint64_t)n, e.drop_thresh, e.drop_scale, v);
+  if (e.drop_thresh) drop4(e.seed, (uint32_t)m * (uint32_t)e.drop_ld + (uint32_t)n, e.drop_thresh, e.drop_scale, v);
   if (e.post_scale) v *= *e.post_scale;
   if (e.aux) {
     f32x4 a = load4<T>((const T*)e.aux + m * e.ldx + n);
@@ -930,6 +930,7 @@ int gemm_launch(const GemmDesc& d, const EpiArgs& e_in, hipStream_t st) {
   if ((d.b_kc && (d.K % 8 || d.ldb % 8)) || (!d.b_kc && (d.N % 8 || d.ldb % 8)))
     return set_error("gemm: B layout needs 8-element aligned rows");
   // epilogue row operand (res / aux) is fetched by 16-byte LDS-DMA pieces
+  if (check_drop_range(e.drop_thresh, (long)d.M * e.drop_ld, "gemm: dropout over >= 2^32 elements")) return -1;
   // The tile epilogue works on 16-byte row pieces (8 bf16): output, pre-activation and the
   // res / aux operand (fetched by LDS-DMA) need 8-element aligned rows.
   auto al8 = [](const void* p, long ld) { return !p || (ld % 8 == 0 && (uintptr_t)p % 16 == 0); };

@@ -100,7 +100,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, l
         if (res) d += load4<T>(res + row * ldr + c * 4);
         store4<T>(dx + row * lddx + c * 4, d);
         if (dxd) {
-          drop4(seed, (uint64_t)row * (uint64_t)D + (uint64_t)(c * 4), thr, dscale, d);
+          drop4(seed, (uint32_t)row * (uint32_t)D + (uint32_t)(c * 4), thr, dscale, d);
           store4<T>(dxd + row * lddx + c * 4, d);
         }
         pg[i] += dyv[i] * xh[i];
@@ -167,6 +167,8 @@ extern "C" int fer_layernorm_bwd(int dtype, const void* dy, int64_t lddy, const 
                                  fer_stream_t stream) {
   if (M <= 0) return 0;
   if (D % 4 || D > 1024) return set_error("layernorm_bwd: D must be a multiple of 4 and <= 1024");
+  if (dx_drop && check_drop_range(drop_thresh, (long)M * D, "layernorm_bwd: dropout over >= 2^32 elements"))
+    return -1;
   if (gamma_rows < 1) gamma_rows = 1;
   if (row_div < 1) row_div = 1;
   const bool want = dgamma || dbeta || dbias;

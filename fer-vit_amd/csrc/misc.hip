@@ -102,7 +102,7 @@ __global__ __launch_bounds__(256) void tokens_fwd_kernel(const T* __restrict__ e
     const int tk = row % N, b = row / N;
     float v = tk == 0 ? cls[d] : to_f<T>(emb[((long)b * n + tk - 1) * D + d]);
     v += pos[(long)tk * D + d];
-    if (thr) v = drop_keep(seed, (uint64_t)i, thr) ? v * dscale : 0.f;
+    if (thr) v = drop_keep(seed, (uint32_t)i, thr) ? v * dscale : 0.f;
     t[i] = from_f<T>(v);
   }
 }
@@ -121,7 +121,7 @@ __global__ __launch_bounds__(256) void tokens_bwd_kernel(const T* __restrict__ d
   for (int b = b0; b < b1; ++b) {
     const long i = (long)b * cols + j;
     float g = to_f<T>(dt[i]);
-    if (thr) g = drop_keep(seed, (uint64_t)i, thr) ? g * dscale : 0.f;
+    if (thr) g = drop_keep(seed, (uint32_t)i, thr) ? g * dscale : 0.f;
     s += g;
     if (tk > 0 && demb) demb[((long)b * n + tk - 1) * D + (j % D)] = from_f<T>(g);
   }
@@ -168,7 +168,7 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(const T* __restrict__ t, 
   const float rsd = rsqrtf((red[4] + red[5] + red[6] + red[7]) / D + eps);
   for (int d = tid; d < D; d += 256) {
     float v = (h[d] - mu) * rsd * lw[d] + lb[d];
-    if (thr) v = drop_keep(seed, (uint64_t)b * D + d, thr) ? v * dscale : 0.f;
+    if (thr) v = drop_keep(seed, (uint32_t)b * (uint32_t)D + (uint32_t)d, thr) ? v * dscale : 0.f;
     h[d] = v;
   }
   __syncthreads();
@@ -203,7 +203,7 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const T* __restrict__ t, 
     const float xhat = (to_f<T>(x[d]) - mu) * rsd;
     float hv = xhat * lw[d] + lb[d];
     bool keep = true;
-    if (thr) keep = drop_keep(seed, (uint64_t)b * D + d, thr);
+    if (thr) keep = drop_keep(seed, (uint32_t)b * (uint32_t)D + (uint32_t)d, thr);
     const float hd = thr ? (keep ? hv * dscale : 0.f) : hv;
     float g = 0.f;
     for (int c = 0; c < C; ++c) {
@@ -578,7 +578,7 @@ template <typename T>
 __global__ void dropout_kernel(const T* __restrict__ x, T* __restrict__ y, long n, uint32_t thr, float sc,
                                uint64_t seed) {
   for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256L)
-    y[i] = from_f<T>(drop_keep(seed, (uint64_t)i, thr) ? to_f<T>(x[i]) * sc : 0.f);
+    y[i] = from_f<T>(drop_keep(seed, (uint32_t)i, thr) ? to_f<T>(x[i]) * sc : 0.f);
 }
 __global__ void clip_coef_kernel(const float* sumsq, float sq_scale, float max_norm, float* coef) {
   if (threadIdx.x) return;
@@ -655,6 +655,7 @@ extern "C" int fer_tokens_fwd(int dtype, const void* emb, const float* cls, cons
                               int D, uint32_t drop_thresh, float drop_scale, uint64_t seed, fer_stream_t stream) {
   const long total = (long)B * (n + 1) * D;
   if (total <= 0) return 0;
+  if (check_drop_range(drop_thresh, total, "tokens_fwd: dropout over >= 2^32 elements")) return -1;
   hipStream_t st = (hipStream_t)stream;
   if (dtype == FER_BF16)
     hipLaunchKernelGGL(tokens_fwd_kernel<bf16>, dim3(grid_for(total)), dim3(256), 0, st, (const bf16*)emb, cls, pos,
@@ -675,6 +676,7 @@ extern "C" int fer_tokens_bwd(int dtype, const void* dt, void* demb, float* dcls
   if (B <= 0) return 0;
   const int nch = tokens_chunks(B);
   if (!ws || ws_bytes < fer_tokens_bwd_ws(B, N, D)) return set_error("tokens_bwd: workspace too small");
+  if (check_drop_range(drop_thresh, (long)B * N * D, "tokens_bwd: dropout over >= 2^32 elements")) return -1;
   const int bchunk = ceil_div(B, nch);
   hipStream_t st = (hipStream_t)stream;
   dim3 grid(ceil_div((long)N * D, 256), nch);
@@ -839,6 +841,7 @@ extern "C" int fer_clip_coef(const float* sumsq, float sq_scale, float max_norm,
 extern "C" int fer_dropout(int dtype, const void* x, void* y, int64_t n, uint32_t drop_thresh, float drop_scale,
                            uint64_t seed, fer_stream_t stream) {
   if (n <= 0) return 0;
+  if (check_drop_range(drop_thresh, n, "dropout: >= 2^32 elements")) return -1;
   hipStream_t st = (hipStream_t)stream;
   if (dtype == FER_BF16)
     hipLaunchKernelGGL(dropout_kernel<bf16>, dim3(grid_for(n)), dim3(256), 0, st, (const bf16*)x, (bf16*)y, (long)n,

@@ -33,10 +33,14 @@ class _Seeds:
     def next(self) -> int:
         if self.base is None:
             self.base = (torch.initial_seed() * 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF
+        # splitmix64: every dropout site gets a fully mixed 64-bit key (the device hash only
+        # xors/adds the key into the element counter before its finaliser, csrc/common.h)
         self.counter += 1
-        z = (self.base + self.counter * 0xBF58476D1CE4E5B9) & 0xFFFFFFFFFFFFFFFF
-        z ^= z >> 31
-        return z
+        m = 0xFFFFFFFFFFFFFFFF
+        z = (self.base + self.counter * 0x9E3779B97F4A7C15) & m
+        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & m
+        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & m
+        return z ^ (z >> 31)
 
 
 SEEDS = _Seeds()

@@ -11,11 +11,11 @@ def _u32(x):
 
 
 def fer_hash(seed: int, pair: np.ndarray) -> np.ndarray:
-    pair = pair.astype(np.uint64)
+    """csrc/common.h fer_hash: x = (pair ^ seed_lo) + seed_hi, then the lowbias32 finaliser."""
+    pair = _u32(pair)
     s_lo, s_hi = np.uint64(seed & 0xFFFFFFFF), np.uint64((seed >> 32) & 0xFFFFFFFF)
     with np.errstate(over="ignore"):
-        x = _u32(_u32(pair) * np.uint64(0x9E3779B1) + s_lo)
-        x = x ^ _u32(_u32(pair >> np.uint64(32)) * np.uint64(0x85EBCA6B) + s_hi)
+        x = _u32((pair ^ s_lo) + s_hi)
         x ^= x >> np.uint64(16)
         x = _u32(x * np.uint64(0x7FEB352D))
         x ^= x >> np.uint64(15)
@@ -30,7 +30,7 @@ def thresh(p: float) -> int:
 
 def keep_mask(seed: int, shape, p: float, base: int = 0) -> torch.Tensor:
     n = int(np.prod(shape))
-    idx = np.arange(base, base + n, dtype=np.uint64)
+    idx = np.arange(base, base + n, dtype=np.uint64) & _M32  # element indices are 32-bit
     h = fer_hash(seed, idx >> np.uint64(1))
     u = (h >> ((idx & np.uint64(1)) * np.uint64(16))) & np.uint64(0xFFFF)
     return torch.from_numpy((u >= np.uint64(thresh(p))).reshape(shape))
