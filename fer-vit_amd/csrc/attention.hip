@@ -17,6 +17,8 @@
 // and the transposed reads:  chunk' = chunk ^ f(row),  f(r) = ((r>>1)&1)<<2 | ((r>>2)&3).
 //
 // fp32 path (parity mode): straightforward kernels over a global [B*H][N][N] workspace.
+#include <stdlib.h>
+
 #include "common.h"
 #include "fervit_internal.h"
 
@@ -385,6 +387,220 @@ __global__ __launch_bounds__(64 * NB) void attn_dkv_bf16(const bf16* __restrict_
   }
 }
 
+// ---------------------------------------------------------------- backward, fused
+// One workgroup per (batch, head), NB waves, wave w owns key block w (K, V fragments in
+// registers, dK / dV accumulators). At step i wave w visits query block qb = (w + i) % NB, so
+// the NB waves always work on NB different query blocks:
+//   S = Q K^T, dP = dO V^T (registers hold queries, lanes hold keys; once per block pair),
+//   P, dS = P o (dropout'(dP) - Dq);  dV += P_drop^T dO;  dK += dS^T Q;
+//   dQ^T(qb) += K^T dS^T: dS goes through a wave-private [key][query] LDS tile and K^T through a
+//   wave-private K image, both read by ds_read_b64_tr_b16;
+//   dQacc[qb] += that partial, after a barrier: the barrier orders the read-modify-writes of
+//   one query block by step index, so the fp32 sum order is fixed (deterministic, no atomics).
+// S, dP, P and the dropout mask are computed once per (query block, key block) instead of once
+// in each of the dQ and dK/dV orientations of the two-kernel path.
+// LDS (NB = 7): Q + dO images 2 x 28 KB, K images 28 KB, dS tiles 14 KB, dQacc fp32 56 KB,
+// lse / Dq 1.75 KB = 155.75 KB -> one workgroup per CU.
+template <int NB>
+constexpr int fused_lds_bytes() {
+  return 3 * NB * 32 * 128 + NB * 2048 + NB * 32 * 64 * 4 + 2 * NB * 32 * 4;
+}
+
+// [32][32] bf16 tile with 64-byte rows (keys x queries): B operand of the 32x32x16 MFMA with
+// lanes = columns (queries) and k = rows rbase + {0..3, 8..11} + 4*(lane>>5) (same k order as
+// rd_tr and the accumulator registers). Four consecutive 64-byte rows per 32-lane half: no
+// bank conflicts without a swizzle.
+FER_DEV bf16x8 rd_tr64(const char* img, int rbase, int lane) {
+  const int gg = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int R = rbase + 4 * (gg >> 1);
+  const int col = 16 * (gg & 1) + 4 * p;
+  const char* a1 = img + (R + q) * 64 + col * 2;
+  const char* a2 = img + (R + 8 + q) * 64 + col * 2;
+  short4_t t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4_t*)a1);
+  short4_t t2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4_t*)a2);
+  bf16x4 b1 = __builtin_bit_cast(bf16x4, t1), b2 = __builtin_bit_cast(bf16x4, t2);
+  return bf16x8{b1[0], b1[1], b1[2], b1[3], b2[0], b2[1], b2[2], b2[3]};
+}
+
+// dQacc: [NB*32 queries][64 d] fp32, 16-byte chunk index XOR (row & 15)
+FER_DEV int dq_off(int row, int chunk) { return row * 256 + ((chunk ^ (row & 15)) << 4); }
+
+template <int NB>
+__global__ __launch_bounds__(64 * NB) void attn_bwd_fused_bf16(const bf16* __restrict__ qkv, long ldq,
+                                                               const bf16* __restrict__ out, long ldo,
+                                                               const bf16* __restrict__ dout, long lddo,
+                                                               const float* __restrict__ lse,
+                                                               bf16* __restrict__ dqkv, long lddq, int N, int H,
+                                                               int dh, float scale, float sl2, uint32_t thr,
+                                                               float dscale, uint64_t seed, int dbg) {
+  constexpr int IMG = NB * 32 * 128;
+  __shared__ __attribute__((aligned(1024))) char lds[fused_lds_bytes<NB>()];
+  char* Qi = lds;
+  char* Oi = lds + IMG;                       // dO image
+  char* Kimg = lds + 2 * IMG;                 // NB x [32 keys][64 d] images
+  char* Sall = lds + 3 * IMG;                 // NB x [32 keys][32 queries] bf16 dS tiles
+  char* dqa = Sall + NB * 2048;               // dQ accumulator
+  float* lse_s = (float*)(dqa + NB * 32 * 64 * 4);
+  float* dd_s = lse_s + NB * 32;
+  const int bh = blockIdx.x, b = bh / H, h = bh - b * H, D = H * dh;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hh = lane >> 5;
+  img_dma<NB>(Qi, make_rsrc(qkv), (long)b * N, ldq, h * dh, N, dh, w, lane);
+  img_dma<NB>(Oi, make_rsrc(dout), (long)b * N, lddo, h * dh, N, dh, w, lane);
+  // zero the dQ accumulator
+  for (int t = threadIdx.x; t < NB * 32 * 16; t += 64 * NB) *(f32x4*)(dqa + t * 16) = f32x4{0.f, 0.f, 0.f, 0.f};
+  // Dq = rowsum(dO o O): two threads per query row
+  for (int t = threadIdx.x; t < NB * 64; t += 64 * NB) {
+    const int qr = t >> 1, half = t & 1;
+    float dsum = 0.f;
+    if (qr < N && !(dbg & 1)) {
+      const bf16* po = out + ((long)b * N + qr) * ldo + h * dh;
+      const bf16* pd = dout + ((long)b * N + qr) * lddo + h * dh;
+      for (int d = half * 8; d < dh; d += 16) {
+        const bf16x8 a = *(const bf16x8*)(po + d), c = *(const bf16x8*)(pd + d);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) dsum += (float)a[j] * (float)c[j];
+      }
+    }
+    dsum += __shfl_xor(dsum, 1, 64);
+    if (!half) {
+      dd_s[qr] = dsum;
+      lse_s[qr] = qr < N ? lse[(long)bh * N + qr] * LOG2E : INFINITY;
+    }
+  }
+  const int key = w * 32 + (lane & 31);
+  const bool kval = key < N;
+  bf16x8 kf[4], vf[4];
+  char* Ki = Kimg + w * 4096;
+  char* Si = Sall + w * 2048;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int d0 = 16 * s + 8 * hh;
+    const bool ok = kval && d0 < dh;
+    kf[s] = ok ? *(const bf16x8*)(qkv + ((long)b * N + key) * ldq + D + h * dh + d0) : bf16x8{};
+    vf[s] = ok ? *(const bf16x8*)(qkv + ((long)b * N + key) * ldq + 2 * D + h * dh + d0) : bf16x8{};
+    // this wave's K block as an LDS image (A operand of dQ^T = K^T dS^T, transposed reads)
+    *(bf16x8*)(Ki + img_off(lane & 31, 2 * s + hh)) = kf[s];
+  }
+  __syncthreads();  // images (DMA: vmcnt(0) + barrier), dQacc zero, lse / Dq visible
+
+  const int NP = N + (N & 1);
+  const bool odd = lane & 1;
+  f32x16 dk[2] = {f32x16{}, f32x16{}}, dv[2] = {f32x16{}, f32x16{}};
+  const int nsteps = (dbg & 2) ? 0 : NB;
+#pragma unroll 1
+  for (int i = 0; i < nsteps; ++i) {
+    int qb = w + i;
+    if (qb >= NB) qb -= NB;
+    f32x16 st = {}, dp = {};
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      st = mfma32(rd_row(Qi, qb * 32 + (lane & 31), 2 * s + hh), kf[s], st);
+      dp = mfma32(rd_row(Oi, qb * 32 + (lane & 31), 2 * s + hh), vf[s], dp);
+    }
+    uint32_t keep = 0xFFFFu;
+    if (thr) {
+      // this lane hashes rows [8*odd, 8*odd + 8) for the key pair (key & ~1, key | 1)
+      uint32_t hv[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int qr = qb * 32 + acc_row(8 * odd + j, hh);
+        hv[j] = fer_hash(seed, (((uint32_t)bh * N + qr) * (uint32_t)NP + (uint32_t)(key & ~1)) >> 1);
+      }
+      keep = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t other = (uint32_t)__shfl_xor((int)hv[j], 1, 64);
+        const uint32_t h_lo = odd ? other : hv[j];  // rows j (even lane's own)
+        const uint32_t h_hi = odd ? hv[j] : other;  // rows 8 + j
+        const uint32_t u_lo = odd ? (h_lo >> 16) : (h_lo & 0xFFFFu);
+        const uint32_t u_hi = odd ? (h_hi >> 16) : (h_hi & 0xFFFFu);
+        keep |= (uint32_t)(u_lo >= thr) << j;
+        keep |= (uint32_t)(u_hi >= thr) << (8 + j);
+      }
+    }
+    // lse / Dq of the 16 query rows of this lane: 4 groups of 4 consecutive rows (one b128 each)
+    f32x4 lq4[4], dq4[4];
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      lq4[g4] = *(const f32x4*)(lse_s + qb * 32 + 8 * g4 + 4 * hh);
+      dq4[g4] = *(const f32x4*)(dd_s + qb * 32 + 8 * g4 + 4 * hh);
+    }
+    f32x16 pd;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      float p = ex2(fmaf(st[r], sl2, -lq4[r >> 2][r & 3]));
+      p = kval ? p : 0.f;
+      const bool kp = (keep >> r) & 1;
+      const float g = thr ? (kp ? dp[r] * dscale : 0.f) : dp[r];
+      pd[r] = thr ? (kp ? p * dscale : 0.f) : p;
+      st[r] = p * (g - dq4[r >> 2][r & 3]);  // dS
+    }
+    // dS tile -> LDS as [key][query] (bf16), read back below as the B operand of dQ^T
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4)
+      *(bf16x4*)(Si + (lane & 31) * 64 + (8 * g4 + 4 * hh) * 2) =
+          bf16x4{(bf16)st[4 * g4], (bf16)st[4 * g4 + 1], (bf16)st[4 * g4 + 2], (bf16)st[4 * g4 + 3]};
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const bf16x8 pf = pack8(pd, s2), df = pack8(st, s2);
+#pragma unroll
+      for (int db = 0; db < 2; ++db) {
+        dv[db] = mfma32(pf, rd_tr(Oi, qb * 32 + 16 * s2, db * 32, lane), dv[db]);
+        dk[db] = mfma32(df, rd_tr(Qi, qb * 32 + 16 * s2, db * 32, lane), dk[db]);
+      }
+    }
+    // dQ^T(qb) partial = K^T dS^T (wave-private LDS: this wave's own writes are visible in order)
+    f32x16 dqt[2] = {f32x16{}, f32x16{}};
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const bf16x8 sf = rd_tr64(Si, 16 * s2, lane);
+#pragma unroll
+      for (int db = 0; db < 2; ++db) dqt[db] = mfma32(rd_tr(Ki, 16 * s2, db * 32, lane), sf, dqt[db]);
+    }
+    // step barrier: the previous visitor of dQacc[qb] (wave w+1, step i-1) has finished
+    __syncthreads();
+    const int qrow = qb * 32 + (lane & 31);
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        f32x4* a = (f32x4*)(dqa + dq_off(qrow, 8 * db + 2 * g4 + hh));
+        *a += f32x4{dqt[db][4 * g4], dqt[db][4 * g4 + 1], dqt[db][4 * g4 + 2], dqt[db][4 * g4 + 3]};
+      }
+  }
+  __syncthreads();  // all dQacc updates done; Q / dO images no longer read
+  // dQ: 16-byte row pieces, scaled
+  for (int t = threadIdx.x; t < NB * 32 * 8; t += 64 * NB) {
+    const int qr = t >> 3, c8 = t & 7;  // 8 d per piece
+    if (qr < N && c8 * 8 < dh) {
+      const f32x4 lo = *(const f32x4*)(dqa + dq_off(qr, 2 * c8)), hi = *(const f32x4*)(dqa + dq_off(qr, 2 * c8 + 1));
+      *(bf16x8*)(dqkv + ((long)b * N + qr) * lddq + h * dh + c8 * 8) =
+          bf16x8{(bf16)(lo[0] * scale), (bf16)(lo[1] * scale), (bf16)(lo[2] * scale), (bf16)(lo[3] * scale),
+                 (bf16)(hi[0] * scale), (bf16)(hi[1] * scale), (bf16)(hi[2] * scale), (bf16)(hi[3] * scale)};
+    }
+  }
+  // dK / dV: stage each wave's 32 x 64 tiles through LDS (reusing the image area) for 16-byte
+  // row stores. dk/dv[db][r]: key row = w*32 + acc_row(r, hh), d = db*32 + (lane&31).
+  bf16* stg = (bf16*)(lds + w * 8192);  // [2][32][64], inside the (now unused) Q / dO images
+#pragma unroll
+  for (int db = 0; db < 2; ++db)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int kr = acc_row(r, hh), d = db * 32 + (lane & 31);
+      stg[kr * 64 + d] = (bf16)(dk[db][r] * scale);
+      stg[2048 + kr * 64 + d] = (bf16)dv[db][r];
+    }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int t = i * 64 + lane;  // 512 chunks of 16 B: [2 mats][32 rows][8 chunks]
+    const int mat = t >> 8, kr = (t >> 3) & 31, c = t & 7;
+    const int gk = w * 32 + kr;
+    if (gk < N && c * 8 < dh)
+      *(bf16x8*)(dqkv + ((long)b * N + gk) * lddq + (1 + mat) * D + h * dh + c * 8) =
+          *(const bf16x8*)(stg + mat * 2048 + kr * 64 + c * 8);
+  }
+}
+
 // ------------------------------------------------------------------ fp32 path
 // ws layout: P [BH][N][N] (softmax probs, undropped), then G [BH][N][N]
 __global__ void attn_f32_scores(const float* qkv, long ldq, float* P, int B, int N, int H, int dh, float scale) {
@@ -545,6 +761,21 @@ extern "C" int fer_attention_bwd(int dtype, const void* qkv, int64_t ld_qkv, con
     return set_error("attention_bwd(bf16): operand exceeds 2 GiB (buffer-resource range)");
   const int nb = (N + 31) / 32;
   const float sl2 = scale * LOG2E;
+  static const bool two_kernel = getenv("FERVIT_ATTN_BWD_2K") != nullptr;  // A/B switch
+  static const int dbg = getenv("FERVIT_ATTN_DBG") ? atoi(getenv("FERVIT_ATTN_DBG")) : 0;  // timing experiments
+  if (nb <= 7 && !two_kernel) {
+#define FER_FUSED(NBV)                                                                                       \
+  case NBV:                                                                                                  \
+    hipLaunchKernelGGL(attn_bwd_fused_bf16<NBV>, dim3(B * H), dim3(64 * NBV), 0, st, (const bf16*)qkv,       \
+                       (long)ld_qkv, (const bf16*)out, (long)ld_out, (const bf16*)dout, (long)ld_dout, lse,   \
+                       (bf16*)dqkv, (long)ld_dqkv, N, H, dh, scale, sl2, drop_thresh, drop_scale, seed, dbg); \
+    break;
+    switch (nb) {  // the fused kernel's LDS fits up to NB = 7 (N <= 224)
+      FER_FUSED(1) FER_FUSED(2) FER_FUSED(3) FER_FUSED(4) FER_FUSED(5) FER_FUSED(6) FER_FUSED(7)
+    }
+#undef FER_FUSED
+    return hip_check("attention_bwd_bf16_fused");
+  }
   FER_NB_SWITCH(nb, hipLaunchKernelGGL(attn_dq_bf16<NB_>, dim3(B * H), dim3(64 * NB_), 0, st, (const bf16*)qkv,
                                        (long)ld_qkv, (const bf16*)out, (long)ld_out, (const bf16*)dout, (long)ld_dout,
                                        lse, (bf16*)dqkv, (long)ld_dqkv, N, H, dh, scale, sl2, drop_thresh, drop_scale,

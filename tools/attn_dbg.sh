@@ -1,0 +1,3 @@
+set -o pipefail
+cd "$GRAFT_REPO_ROOT/tools" && mkdir -p ../gpurun_out
+for d in 0 1 2 3; do echo "== dbg $d"; FERVIT_ATTN_DBG=$d timeout -k 10 120 python -u attn_bench.py 2>&1 | grep -v amdgpu.ids || exit 1; done | tee ../gpurun_out/attndbg_$1.txt
