@@ -40,6 +40,12 @@ template <> FER_DEV f32x4 load4<bf16>(const bf16* p) {
   bf16x4 v = *(const bf16x4*)p;
   return f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
 }
+// Raw (unconverted) 4-element vectors, for loads whose conversion is deferred to the use.
+template <typename T> struct Raw4;
+template <> struct Raw4<float> { typedef f32x4 type; };
+template <> struct Raw4<bf16> { typedef bf16x4 type; };
+FER_DEV f32x4 raw4_to_f(f32x4 v) { return v; }
+FER_DEV f32x4 raw4_to_f(bf16x4 v) { return f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]}; }
 template <typename T> FER_DEV void store4(T* p, f32x4 v);
 template <> FER_DEV void store4<float>(float* p, f32x4 v) { *(f32x4*)p = v; }
 template <> FER_DEV void store4<bf16>(bf16* p, f32x4 v) {

@@ -71,7 +71,23 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, l
   f32x4 pg[LN_VPL], pb[LN_VPL], pd[LN_VPL];
 #pragma unroll
   for (int i = 0; i < LN_VPL; ++i) pg[i] = pb[i] = pd[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (long row = (long)blockIdx.x * 4 + w; row < M; row += (long)gridDim.x * 4) {
+  // Rows are processed in pairs with two register sets: the loads of the next row are issued
+  // before the stores of the current one. (vmcnt retires loads and stores in issue order: a
+  // load issued after a store would make every use wait for that store to drain.)
+  typedef typename Raw4<T>::type R4;
+  R4 dyA[LN_VPL], xA[LN_VPL], rA[LN_VPL], dyB[LN_VPL], xB[LN_VPL], rB[LN_VPL];
+  auto load_row = [&](long row, R4(&dyr)[LN_VPL], R4(&xr)[LN_VPL], R4(&rr)[LN_VPL]) {
+#pragma unroll
+    for (int i = 0; i < LN_VPL; ++i) {
+      const int c = lane + i * 64;
+      if (c < nv) {
+        dyr[i] = *(const R4*)(dy + row * lddy + c * 4);
+        xr[i] = *(const R4*)(x + row * ldx + c * 4);
+        if (res) rr[i] = *(const R4*)(res + row * ldr + c * 4);
+      }
+    }
+  };
+  auto proc_row = [&](long row, const R4(&dyr)[LN_VPL], const R4(&xr)[LN_VPL], const R4(&rr)[LN_VPL]) {
     const float mu = mean[row], rs = rstd[row];
     const long gr = grows > 1 ? ((row / rdiv) % grows) * D : 0;
     f32x4 xh[LN_VPL], gy[LN_VPL], dyv[LN_VPL];
@@ -80,8 +96,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, l
     for (int i = 0; i < LN_VPL; ++i) {
       const int c = lane + i * 64;
       if (c < nv) {
-        dyv[i] = load4<T>(dy + row * lddy + c * 4);
-        xh[i] = (load4<T>(x + row * ldx + c * 4) - mu) * rs;
+        dyv[i] = raw4_to_f(dyr[i]);
+        xh[i] = (raw4_to_f(xr[i]) - mu) * rs;
         gy[i] = dyv[i] * *(const f32x4*)(g + gr + c * 4);
         s1 += gy[i][0] + gy[i][1] + gy[i][2] + gy[i][3];
         f32x4 t = gy[i] * xh[i];
@@ -97,7 +113,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, l
       const int c = lane + i * 64;
       if (c < nv) {
         f32x4 d = (gy[i] - s1 - xh[i] * s2) * rs;
-        if (res) d += load4<T>(res + row * ldr + c * 4);
+        if (res) d += raw4_to_f(rr[i]);
         store4<T>(dx + row * lddx + c * 4, d);
         if (dxd) {
           drop4(seed, (uint32_t)row * (uint32_t)D + (uint32_t)(c * 4), thr, dscale, d);
@@ -108,6 +124,17 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, l
         pd[i] += d;
       }
     }
+  };
+  const long stride = (long)gridDim.x * 4;
+  long row = (long)blockIdx.x * 4 + w;
+  if (row < M) load_row(row, dyA, xA, rA);
+  for (; row < M; row += 2 * stride) {
+    const long r2 = row + stride;
+    if (r2 < M) load_row(r2, dyB, xB, rB);
+    proc_row(row, dyA, xA, rA);
+    if (r2 >= M) break;
+    if (r2 + stride < M) load_row(r2 + stride, dyA, xA, rA);
+    proc_row(r2, dyB, xB, rB);
   }
   if (!want_part) return;
 #pragma unroll

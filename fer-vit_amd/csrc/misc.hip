@@ -19,16 +19,18 @@ __global__ __launch_bounds__(256) void part_reduce_kernel(const float* __restric
   __shared__ float red[8][33];
   const int cx = threadIdx.x & 31, j = threadIdx.x >> 5;
   const int c = blockIdx.x * 32 + cx;
-  float s0 = 0.f, s1 = 0.f;
+  // 8 independent accumulators: 8 loads in flight per thread (the partial slabs are read once,
+  // the sum is latency-bound otherwise). Fixed association order -> deterministic.
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if (c < ncols) {
     int b = j;
-    for (; b + 8 < nb; b += 16) {
-      s0 += part[(long)b * ld + c];
-      s1 += part[(long)(b + 8) * ld + c];
+    for (; b + 56 < nb; b += 64) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s[u] += part[(long)(b + 8 * u) * ld + c];
     }
-    if (b < nb) s0 += part[(long)b * ld + c];
+    for (int u = 0; b < nb; b += 8, ++u) s[u] += part[(long)b * ld + c];
   }
-  red[j][cx] = s0 + s1;
+  red[j][cx] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
   __syncthreads();
   if (j == 0 && c < ncols) {
     float t = 0.f;
