@@ -432,7 +432,8 @@ __global__ __launch_bounds__(64 * NB) void attn_bwd_fused_bf16(const bf16* __res
                                                                const float* __restrict__ lse,
                                                                bf16* __restrict__ dqkv, long lddq, int N, int H,
                                                                int dh, float scale, float sl2, uint32_t thr,
-                                                               float dscale, uint64_t seed, int dbg) {
+                                                               float dscale, uint64_t seed, float* __restrict__ cs_part,
+                                                               int dbg) {
   constexpr int IMG = NB * 32 * 128;
   __shared__ __attribute__((aligned(1024))) char lds[fused_lds_bytes<NB>()];
   char* Qi = lds;
@@ -579,6 +580,38 @@ __global__ __launch_bounds__(64 * NB) void attn_bwd_fused_bf16(const bf16* __res
                  (bf16)(hi[0] * scale), (bf16)(hi[1] * scale), (bf16)(hi[2] * scale), (bf16)(hi[3] * scale)};
     }
   }
+  if (cs_part) {
+    // in_proj.bias gradient partials of batch b: column sums of dq (from dQacc), dk, dv (from
+    // the accumulators) over this head's rows, in a fixed order. Scratch: the K-image area.
+    float* red = (float*)Kimg;  // [NB][3][64]
+    {  // dQ: wave w sums rows w, w+NB, ... of column d = lane
+      float t = 0.f;
+      for (int r = w; r < NB * 32; r += NB) t += ((const float*)(dqa + dq_off(r, lane >> 2)))[lane & 3];
+      red[w * 192 + lane] = t * scale;
+    }
+#pragma unroll
+    for (int db = 0; db < 2; ++db) {  // dK / dV: 16 key rows per lane, + the other half-wave
+      float tk = 0.f, tv = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        tk += dk[db][r];
+        tv += dv[db][r];
+      }
+      tk += __shfl_xor(tk, 32, 64);
+      tv += __shfl_xor(tv, 32, 64);
+      if (hh == 0) {
+        red[w * 192 + 64 + db * 32 + lane] = tk * scale;
+        red[w * 192 + 128 + db * 32 + lane] = tv;
+      }
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < 192; c += 64 * NB) {
+      float t = 0.f;
+      for (int j = 0; j < NB; ++j) t += red[j * 192 + c];
+      const int mat = c >> 6, d = c & 63;
+      if (d < dh) cs_part[(long)b * 3 * D + mat * D + h * dh + d] = t;
+    }
+  }
   // dK / dV: stage each wave's 32 x 64 tiles through LDS (reusing the image area) for 16-byte
   // row stores. dk/dv[db][r]: key row = w*32 + acc_row(r, hh), d = db*32 + (lane&31).
   bf16* stg = (bf16*)(lds + w * 8192);  // [2][32][64], inside the (now unused) Q / dO images
@@ -700,7 +733,10 @@ __global__ void attn_f32_grads(const float* P, const float* G, const float* qkv,
 using namespace fer;
 
 extern "C" int64_t fer_attention_ws(int dtype, int B, int N, int H) {
-  return dtype == FER_F32 ? (int64_t)2 * B * H * N * N * 4 : 0;
+  // fp32 path: P and dS slabs, then the stand-alone colsum pass's partials; bf16: the fused
+  // bias-gradient partials [B][3*H*64]
+  const int64_t cs = std::max<int64_t>(fer_colsum_ws(B * N, 3 * H * 64), (int64_t)B * 3 * H * 64 * 4);
+  return (dtype == FER_F32 ? (int64_t)2 * B * H * N * N * 4 : 0) + cs;
 }
 
 extern "C" int fer_attention_fwd(int dtype, const void* qkv, int64_t ld_qkv, void* out, int64_t ld_out, float* lse,
@@ -734,9 +770,17 @@ extern "C" int fer_attention_fwd(int dtype, const void* qkv, int64_t ld_qkv, voi
 extern "C" int fer_attention_bwd(int dtype, const void* qkv, int64_t ld_qkv, const void* out, int64_t ld_out,
                                  const void* dout, int64_t ld_dout, const float* lse, void* dqkv, int64_t ld_dqkv,
                                  float* ws, int64_t ws_bytes, int B, int N, int H, int dh, float scale,
-                                 uint32_t drop_thresh, float drop_scale, uint64_t seed, fer_stream_t stream) {
+                                 uint32_t drop_thresh, float drop_scale, uint64_t seed, float* colsum,
+                                 int colsum_accumulate, fer_stream_t stream) {
   if (B <= 0) return 0;
   hipStream_t st = (hipStream_t)stream;
+  const int D3 = 3 * H * dh;
+  if (colsum && (!ws || ws_bytes < fer_attention_ws(dtype, B, N, H)))
+    return set_error("attention_bwd: colsum needs the workspace (fer_attention_ws bytes)");
+  // column sums of dqkv by a separate pass (fp32 path, two-kernel bf16 path)
+  auto colsum_pass = [&](float* cws, int64_t cbytes) -> int {
+    return fer_colsum(dtype, dqkv, ld_dqkv, B * N, D3, colsum, colsum_accumulate, nullptr, cws, cbytes, stream);
+  };
   if (dtype == FER_F32) {
     if (!ws || ws_bytes < fer_attention_ws(dtype, B, N, H)) return set_error("attention_bwd: fp32 workspace too small");
     const long pe = (long)B * H * N * N, rows = (long)B * H * N, oe = rows * dh;
@@ -751,7 +795,9 @@ extern "C" int fer_attention_bwd(int dtype, const void* qkv, int64_t ld_qkv, con
     hipLaunchKernelGGL(attn_f32_grads, dim3(ceil_div(oe, 256)), dim3(256), 0, st, (const float*)P, (const float*)G,
                        (const float*)qkv, (long)ld_qkv, (const float*)dout, (long)ld_dout, (float*)dqkv,
                        (long)ld_dqkv, B, N, H, dh, scale, drop_thresh, drop_scale, seed);
-    return hip_check("attention_bwd_f32");
+    int rc = hip_check("attention_bwd_f32");
+    if (rc || !colsum) return rc;
+    return colsum_pass(ws + 2 * pe, ws_bytes - 2 * pe * 4);
   }
   if (N > 256 || dh > 64 || dh % 8) return set_error("attention_bwd(bf16): needs N <= 256, dh <= 64, dh % 8 == 0");
   if (check_drop_range(drop_thresh, (long)B * H * N * (N + (N & 1)), "attention_bwd: dropout over >= 2^32 probabilities"))
@@ -768,13 +814,17 @@ extern "C" int fer_attention_bwd(int dtype, const void* qkv, int64_t ld_qkv, con
   case NBV:                                                                                                  \
     hipLaunchKernelGGL(attn_bwd_fused_bf16<NBV>, dim3(B * H), dim3(64 * NBV), 0, st, (const bf16*)qkv,       \
                        (long)ld_qkv, (const bf16*)out, (long)ld_out, (const bf16*)dout, (long)ld_dout, lse,   \
-                       (bf16*)dqkv, (long)ld_dqkv, N, H, dh, scale, sl2, drop_thresh, drop_scale, seed, dbg); \
+                       (bf16*)dqkv, (long)ld_dqkv, N, H, dh, scale, sl2, drop_thresh, drop_scale, seed,      \
+                       colsum ? ws : nullptr, dbg);                                                         \
     break;
     switch (nb) {  // the fused kernel's LDS fits up to NB = 7 (N <= 224)
       FER_FUSED(1) FER_FUSED(2) FER_FUSED(3) FER_FUSED(4) FER_FUSED(5) FER_FUSED(6) FER_FUSED(7)
     }
 #undef FER_FUSED
-    return hip_check("attention_bwd_bf16_fused");
+    int rc = hip_check("attention_bwd_bf16_fused");
+    if (rc || !colsum) return rc;
+    part_reduce(ws, B, D3, D3, D3, colsum, nullptr, nullptr, colsum_accumulate, nullptr, st);
+    return hip_check("attention_bwd_colsum");
   }
   FER_NB_SWITCH(nb, hipLaunchKernelGGL(attn_dq_bf16<NB_>, dim3(B * H), dim3(64 * NB_), 0, st, (const bf16*)qkv,
                                        (long)ld_qkv, (const bf16*)out, (long)ld_out, (const bf16*)dout, (long)ld_dout,
@@ -784,5 +834,7 @@ extern "C" int fer_attention_bwd(int dtype, const void* qkv, int64_t ld_qkv, con
                                    (long)ld_qkv, (const bf16*)out, (long)ld_out, (const bf16*)dout, (long)ld_dout,
                                    lse, (bf16*)dqkv, (long)ld_dqkv, N, H, dh, scale, sl2, drop_thresh, drop_scale,
                                    seed));
-  return hip_check("attention_bwd_bf16");
+  int rc = hip_check("attention_bwd_bf16");
+  if (rc || !colsum) return rc;
+  return colsum_pass(ws, ws_bytes);
 }

@@ -19,6 +19,7 @@ struct GemmArgs {
   int tiles_m, tiles_n;
   int splits, k_chunk, partial;
   float* ws;
+  float* cs_part;  // fused column sums: per-tile partials [tiles_m][N] (or null)
   int dbg;  // experiment switches (FERVIT_GEMM_DBG), 0 in production
 };
 

@@ -40,7 +40,7 @@ FER_DEV f32x4 hi4(bf16x8 x) { return f32x4{(float)x[4], (float)x[5], (float)x[6]
 FER_DEV bf16x8 pack8(f32x4 a, f32x4 b) {
   return bf16x8{(bf16)a[0], (bf16)a[1], (bf16)a[2], (bf16)a[3], (bf16)b[0], (bf16)b[1], (bf16)b[2], (bf16)b[3]};
 }
-FER_DEV void epi8_bf16(const EpiArgs& e, long m, long n, f32x4 v0, f32x4 v1, f32x4 b0, f32x4 b1, bf16x8 x,
+FER_DEV void epi8_bf16(const EpiArgs& e, long m, long n, f32x4& v0, f32x4& v1, f32x4 b0, f32x4 b1, bf16x8 x,
                        float ps) {
   v0 = v0 * e.alpha + b0;
   v1 = v1 * e.alpha + b1;
@@ -372,15 +372,20 @@ FER_DEV void tile_epilogue(const GemmArgs& g, const EpiArgs& e, AccT (&acc)[FN][
     }
     __syncthreads();  // staging and X[h&1] (all waves' DMA) visible
   };
+  f32x4 cs0 = f32x4{0.f, 0.f, 0.f, 0.f}, cs1 = cs0;  // fused column sums of this thread's rows
   auto finish = [&](int h) {
     const char* xh = xb + (h & 1) * XBYTES;
 #pragma unroll 1
     for (int it = 0; it < IT; ++it) {
       const int r = tr + it * RPI;
       const long m = m0 + h * EROWS + r;
-      const f32x4 v0 = *(const f32x4*)(stg + swz(r, tc)), v1 = *(const f32x4*)(stg + swz(r, tc + 4));
+      f32x4 v0 = *(const f32x4*)(stg + swz(r, tc)), v1 = *(const f32x4*)(stg + swz(r, tc + 4));
       const bf16x8 x = xs ? *(const bf16x8*)(xh + (r * BN + tc) * 2) : bf16x8{};
-      if (nok && m < g.M) epi8_bf16(e, m, n, v0, v1, b0, b1, x, ps);
+      if (nok && m < g.M) {
+        epi8_bf16(e, m, n, v0, v1, b0, b1, x, ps);
+        cs0 += v0;
+        cs1 += v1;
+      }
     }
   };
   if (xs) issue_x(0);
@@ -391,6 +396,18 @@ FER_DEV void tile_epilogue(const GemmArgs& g, const EpiArgs& e, AccT (&acc)[FN][
     finish(h0);
     stage(h1, h1 / EPC, EPC == 2 ? 1 : 0);
     finish(h1);
+  }
+  if (g.cs_part) {  // column partial sums of this tile -> cs_part[tile row][n], fixed order
+    __syncthreads();  // staging area free
+    float* red = (float*)smem;  // [RPI][BN]
+    *(f32x4*)(red + tr * BN + tc) = cs0;
+    *(f32x4*)(red + tr * BN + tc + 4) = cs1;
+    __syncthreads();
+    for (int c = threadIdx.x; c < BN; c += NT) {
+      float t = 0.f;
+      for (int r = 0; r < RPI; ++r) t += red[r * BN + c];
+      if (n0 + c < g.N) g.cs_part[(long)(m0 / BM) * g.N + n0 + c] = t;
+    }
   }
 }
 
@@ -921,12 +938,20 @@ int gemm_launch(const GemmDesc& d, const EpiArgs& e_in, hipStream_t st) {
   g.dbg = dbg;
   if (d.M <= 0 || d.N <= 0) return 0;
   if (d.N % 4) return set_error("gemm: N must be a multiple of 4");
+  if (e.colsum && (!d.ws || d.ws_bytes < fer_gemm_colsum_ws(d.M, d.N)))
+    return set_error("gemm: fused column sums need the desc workspace (fer_gemm_colsum_ws bytes)");
+  // column sums of the output by a separate pass (fp32 parity path)
+  auto colsum_pass = [&]() -> int {
+    return fer_colsum(e.c_f32 ? FER_F32 : d.dtype, e.c, e.ldc, d.M, d.N, e.colsum, e.colsum_accumulate, nullptr,
+                      d.ws, d.ws_bytes, (fer_stream_t)st);
+  };
   if (d.dtype == FER_F32) {
     g.tiles_m = (d.M + 63) / 64;
     g.tiles_n = (d.N + 63) / 64;
     g.splits = 1;
     hipLaunchKernelGGL(gemm_f32_kernel, dim3(g.tiles_m * g.tiles_n), dim3(256), 0, st, g, e, d.a_kc, d.b_kc);
-    return hip_check("gemm_f32");
+    int rc = hip_check("gemm_f32");
+    return (rc || !e.colsum) ? rc : colsum_pass();
   }
   // bf16: alignment contract of the DMA staging (16-byte chunks)
   if ((d.a_kc && (d.K % 8 || d.lda % 8)) || (!d.a_kc && (d.M % 8 || d.lda % 8)))
@@ -950,7 +975,8 @@ int gemm_launch(const GemmDesc& d, const EpiArgs& e_in, hipStream_t st) {
   // Split-K (weight gradients, K = tokens) targets one 256^2 workgroup per CU.
   const long t256 = (long)((d.M + 255) / 256) * ((d.N + 255) / 256);
   const long t128 = (long)((d.M + 127) / 128) * ((d.N + 127) / 128);
-  const int max_splits = d.ws ? (int)std::min<long>(64, d.ws_bytes / ((long)d.M * d.N * 4)) : 1;
+  // (fused column sums use the workspace for their tile partials: no split-K then)
+  const int max_splits = (d.ws && !e.colsum) ? (int)std::min<long>(64, d.ws_bytes / ((long)d.M * d.N * 4)) : 1;
   auto splits_for = [&](long tiles, long target) -> int {
     if (max_splits < 2 || d.K < 1024 || tiles >= target) return 1;
     return (int)std::max<long>(1, std::min<long>({target / tiles, d.K / 256, (long)max_splits}));
@@ -963,12 +989,19 @@ int gemm_launch(const GemmDesc& d, const EpiArgs& e_in, hipStream_t st) {
   if (splits > 1) g.splits = (d.K + g.k_chunk - 1) / g.k_chunk;
   g.partial = g.splits > 1;
   g.ws = d.ws;
+  g.cs_part = e.colsum ? d.ws : nullptr;
 
   if (d.a_kc && d.b_kc) dispatch_tile<true, true>(cfg, g, e, st);
   else if (d.a_kc && !d.b_kc) dispatch_tile<true, false>(cfg, g, e, st);
   else if (!d.a_kc && !d.b_kc) dispatch_tile<false, false>(cfg, g, e, st);
   else dispatch_tile<false, true>(cfg, g, e, st);
   int rc = hip_check("gemm_bf16");
+  if (!rc && e.colsum) {  // fixed-order reduction of the per-tile column partials
+    const int bm = cfg_is_256(cfg) ? 256 : 128;
+    part_reduce(d.ws, (d.M + bm - 1) / bm, d.N, d.N, d.N, e.colsum, nullptr, nullptr, e.colsum_accumulate, nullptr,
+                st);
+    rc = hip_check("gemm_colsum_reduce");
+  }
   if (rc || !g.partial) return rc;
   const long work = (long)d.M * (d.N / 4);
   const int blocks = (int)std::min<long>((work + 255) / 256, 4096);
@@ -978,6 +1011,11 @@ int gemm_launch(const GemmDesc& d, const EpiArgs& e_in, hipStream_t st) {
 }
 
 }  // namespace fer
+
+extern "C" int64_t fer_gemm_colsum_ws(int M, int N) {
+  // tile partials (128-row tiles at most) or the stand-alone colsum pass's partials
+  return (int64_t)std::max(fer::ceil_div(std::max(M, 1), 128), 256) * N * 4;
+}
 
 extern "C" int fer_gemm_set_config(int cfg) {
   if (cfg < -1 || cfg > 9) return fer::set_error("gemm_set_config: cfg must be -1 (automatic) or 0..9");

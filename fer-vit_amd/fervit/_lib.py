@@ -29,7 +29,8 @@ class Epilogue(C.Structure):
     _fields_ = [("c", vp), ("ldc", i64), ("c_f32", i32), ("accumulate", i32), ("alpha", f32),
                 ("bias", vp), ("act", i32), ("pre", vp), ("ldp", i64), ("res", vp), ("ldr", i64),
                 ("drop_thresh", u32), ("drop_scale", f32), ("seed", u64), ("drop_ld", i64),
-                ("aux", vp), ("ldx", i64), ("aux_act", i32), ("post_scale", vp)]
+                ("aux", vp), ("ldx", i64), ("aux_act", i32), ("post_scale", vp), ("colsum", vp),
+                ("colsum_accumulate", i32)]
 
 
 class AdamWSegment(C.Structure):
@@ -41,6 +42,7 @@ class AdamWSegment(C.Structure):
 SIGNATURES = {
     "fer_gemm": (i32, [C.POINTER(GemmDesc), C.POINTER(Epilogue), vp]),
     "fer_gemm_set_config": (i32, [i32]),
+    "fer_gemm_colsum_ws": (i64, [i32, i32]),
     "fer_layernorm_fwd": (i32, [i32, vp, i64, fp, fp, i32, i32, vp, i64, fp, fp, i32, i32, f32, vp]),
     "fer_layernorm_bwd_ws": (i64, [i32, i32]),
     "fer_layernorm_bwd": (i32, [i32, vp, i64, vp, i64, fp, fp, fp, i32, i32, vp, i64, vp, i64, vp, u32, f32, u64,
@@ -48,7 +50,7 @@ SIGNATURES = {
     "fer_attention_ws": (i64, [i32, i32, i32, i32]),
     "fer_attention_fwd": (i32, [i32, vp, i64, vp, i64, fp, i32, i32, i32, i32, f32, u32, f32, u64, fp, i64, vp]),
     "fer_attention_bwd": (i32, [i32, vp, i64, vp, i64, vp, i64, fp, vp, i64, fp, i64, i32, i32, i32, i32, f32, u32,
-                                f32, u64, vp]),
+                                f32, u64, fp, i32, vp]),
     "fer_colsum_ws": (i64, [i32, i32]),
     "fer_colsum": (i32, [i32, vp, i64, i32, i32, fp, i32, fp, fp, i64, vp]),
     "fer_im2col_patch": (i32, [i32, fp, i32, i32, i32, i32, i32, vp, i64, vp]),

@@ -125,10 +125,9 @@ class PostNormLayerFn(torch.autograd.Function):
         dh2 = dz if dh2 is None else dh2
         if gw2 is not None:
             ops.linear_wgrad(dh2, g, gw2, accumulate=acc)
+        # linear1.bias grad = column sums of dF, fused into this GEMM's epilogue
         dF = ops.linear_dgrad(dh2, _weight(flat, w2, dt), dropout=pd, seed=seeds[2], drop_ld=w1.shape[0], aux=f,
-                              aux_act=cfg.act)
-        if gb1 is not None:
-            ops.colsum(dF, gb1, accumulate=acc)
+                              aux_act=cfg.act, colsum=gb1, colsum_accumulate=acc)
         if gw1 is not None:
             ops.linear_wgrad(dF, x1, gw1, accumulate=acc)
         dx1 = ops.linear_dgrad(dF, _weight(flat, w1, dt), res=dz)
@@ -142,9 +141,8 @@ class PostNormLayerFn(torch.autograd.Function):
             ops.linear_wgrad(dhh, o, gout_w, accumulate=acc)
         do = ops.linear_dgrad(dhh, _weight(flat, out_w, dt))
         dqkv = _empty(M, 3 * D, x)
-        ops.attention_bwd(qkv, o, do, lse, dqkv, cfg.B, cfg.N, cfg.H, dh, dropout=pd, seed=seeds[0])
-        if gin_b is not None:
-            ops.colsum(dqkv, gin_b, accumulate=acc)
+        ops.attention_bwd(qkv, o, do, lse, dqkv, cfg.B, cfg.N, cfg.H, dh, dropout=pd, seed=seeds[0], colsum=gin_b,
+                          colsum_accumulate=acc)
         if gin_w is not None:
             ops.linear_wgrad(dqkv, x, gin_w, accumulate=acc)
         dx = ops.linear_dgrad(dqkv, _weight(flat, in_w, dt), res=dy)
@@ -199,9 +197,8 @@ class PreNormBlockFn(torch.autograd.Function):
             ops.colsum(dout, gfc2_b, accumulate=acc)
         if gfc2_w is not None:
             ops.linear_wgrad(dout, g, gfc2_w, accumulate=acc)
-        dF = ops.linear_dgrad(dout, _weight(flat, fc2_w, dt), aux=f, aux_act="gelu")
-        if gfc1_b is not None:
-            ops.colsum(dF, gfc1_b, accumulate=acc)
+        dF = ops.linear_dgrad(dout, _weight(flat, fc2_w, dt), aux=f, aux_act="gelu", colsum=gfc1_b,
+                              colsum_accumulate=acc)
         if gfc1_w is not None:
             ops.linear_wgrad(dF, h2, gfc1_w, accumulate=acc)
         dh2 = ops.linear_dgrad(dF, _weight(flat, fc1_w, dt))
@@ -212,9 +209,7 @@ class PreNormBlockFn(torch.autograd.Function):
             ops.linear_wgrad(dx2, o, gproj_w, accumulate=acc)
         do = ops.linear_dgrad(dx2, _weight(flat, proj_w, dt))
         dqkv = _empty(M, 3 * D, x)
-        ops.attention_bwd(qkv, o, do, lse, dqkv, cfg.B, cfg.N, cfg.H, dh)
-        if gqkv_b is not None:
-            ops.colsum(dqkv, gqkv_b, accumulate=acc)
+        ops.attention_bwd(qkv, o, do, lse, dqkv, cfg.B, cfg.N, cfg.H, dh, colsum=gqkv_b, colsum_accumulate=acc)
         if gqkv_w is not None:
             ops.linear_wgrad(dqkv, h1, gqkv_w, accumulate=acc)
         dh1 = ops.linear_dgrad(dqkv, _weight(flat, qkv_w, dt))

@@ -77,8 +77,10 @@ def gemm(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, *, a_kc: bool = Tr
          bias: Optional[torch.Tensor] = None, act: str = "none", pre: Optional[torch.Tensor] = None,
          res: Optional[torch.Tensor] = None, dropout: float = 0.0, seed: int = 0, drop_ld: Optional[int] = None,
          aux: Optional[torch.Tensor] = None, aux_act: str = "none", alpha: float = 1.0, accumulate: bool = False,
-         post_scale: Optional[torch.Tensor] = None, split_ws: bool = True) -> torch.Tensor:
-    """out[m][n] = epilogue(sum_k A(m,k) B(n,k)); see include/fervit.h for the layouts."""
+         post_scale: Optional[torch.Tensor] = None, split_ws: bool = True,
+         colsum: Optional[torch.Tensor] = None, colsum_accumulate: bool = False) -> torch.Tensor:
+    """out[m][n] = epilogue(sum_k A(m,k) B(n,k)); see include/fervit.h for the layouts.
+    colsum: optional fp32 [N] receiving (or, with colsum_accumulate, adding) sum_m out[m][n]."""
     _dev(A)
     if A.dtype != B.dtype:
         raise TypeError("gemm: A and B dtypes differ")
@@ -90,7 +92,10 @@ def gemm(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, *, a_kc: bool = Tr
     d.a_kc, d.b_kc = int(a_kc), int(b_kc)
     d.M, d.N, d.K = M, N, K
     t256 = -(-M // 256) * -(-N // 256)
-    if split_ws and d.dtype == 0 and K >= 1024 and t256 < 256:
+    if colsum is not None:
+        w = WS.get(lib().fer_gemm_colsum_ws(M, N), A.device, slot=1)
+        d.ws, d.ws_bytes = w.data_ptr(), w.numel() * 4
+    elif split_ws and d.dtype == 0 and K >= 1024 and t256 < 256:
         # split-K slabs: the library targets ~one 256x256 workgroup per CU (or 512 128^2 ones)
         nb = 4 * M * N * min(32, max(2, 512 // t256))
         w = WS.get(nb, A.device, slot=1)
@@ -114,6 +119,8 @@ def gemm(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, *, a_kc: bool = Tr
     e.ldx = N if aux is None else aux.stride(0)
     e.aux_act = ACT[aux_act]
     e.post_scale = ptr(post_scale)
+    e.colsum = ptr(colsum)
+    e.colsum_accumulate = int(colsum_accumulate)
     if LAUNCH_PROBE is not None:
         LAUNCH_PROBE(d, lambda: check(lib().fer_gemm(C_ref(d), C_ref(e), stream()), "gemm"))
     else:
@@ -189,14 +196,18 @@ def attention_fwd(qkv, out, lse, B, N, H, dh, dropout=0.0, seed=0):
     return out
 
 
-def attention_bwd(qkv, out, dout, lse, dqkv, B, N, H, dh, dropout=0.0, seed=0):
+def attention_bwd(qkv, out, dout, lse, dqkv, B, N, H, dh, dropout=0.0, seed=0, colsum=None,
+                  colsum_accumulate=False):
+    """dqkv = d(attention)/d(qkv); colsum (fp32 [3*H*dh], optional) (+)= column sums of dqkv
+    (the in_proj bias gradient), fused into the backward kernel."""
     thr, sc = drop_args(dropout)
     nb = lib().fer_attention_ws(dcode(qkv), B, N, H)
     ws = WS.get(nb, qkv.device) if nb else None
     check(lib().fer_attention_bwd(dcode(qkv), qkv.data_ptr(), qkv.stride(0), out.data_ptr(), out.stride(0),
                                   dout.data_ptr(), dout.stride(0), lse.data_ptr(), dqkv.data_ptr(), dqkv.stride(0),
                                   ptr(ws), 0 if ws is None else ws.numel() * 4, B, N, H, dh, 1.0 / math.sqrt(dh),
-                                  thr, sc, seed & (2**64 - 1), stream()), "attention_bwd")
+                                  thr, sc, seed & (2**64 - 1), ptr(colsum), int(colsum_accumulate), stream()),
+          "attention_bwd")
     return dqkv
 
 

@@ -58,9 +58,17 @@ typedef struct {
   uint32_t drop_thresh; float drop_scale; uint64_t seed; int64_t drop_ld;
   const void* aux; int64_t ldx; int aux_act;
   const float* post_scale;
+  /* optional fp32 column sums of the final output (the bias gradient of a layer whose input
+   * gradient this GEMM produces, e.g. linear1.bias from the linear2 dgrad): colsum[n] (+)=
+   * sum_m c[m][n]. Fused into the tile epilogue (per-tile partials + a fixed-order reduction,
+   * deterministic); needs the desc workspace ws (>= fer_gemm_colsum_ws bytes). */
+  float* colsum; int colsum_accumulate;
 } fer_epilogue;
 
 int fer_gemm(const fer_gemm_desc* d, const fer_epilogue* e, fer_stream_t stream);
+
+/* Workspace bytes fer_gemm needs for the fused column sums of an M x N output. */
+int64_t fer_gemm_colsum_ws(int M, int N);
 
 /* Tuning/testing hook (no reference counterpart): force the bf16 GEMM tile configuration for
  * every later fer_gemm call of the process. -1 = automatic (default); 0..9 = fixed kernel
@@ -93,16 +101,18 @@ int fer_layernorm_bwd(int dtype, const void* dy, int64_t lddy, const void* x, in
  * probabilities (F.multi_head_attention_forward -> scaled_dot_product_attention inside
  * nn.TransformerEncoderLayer; timm Attention for the hybrid). qkv: [B*N][ld_qkv] with
  * q|k|v column blocks of width H*dh (in_proj rows order); out: [B*N][ld_out].
- * lse [B*H*N] fp32 is saved for backward. N <= 256, dh <= 128, dh % 16 == 0 (bf16). */
+ * lse [B*H*N] fp32 is saved for backward. bf16: N <= 256, dh <= 64, dh % 8 == 0. */
 int64_t fer_attention_ws(int dtype, int B, int N, int H);
 int fer_attention_fwd(int dtype, const void* qkv, int64_t ld_qkv, void* out, int64_t ld_out, float* lse, int B,
                       int N, int H, int dh, float scale, uint32_t drop_thresh, float drop_scale, uint64_t seed,
                       float* ws, int64_t ws_bytes, fer_stream_t stream);
-/* Backward: dqkv [B*N][ld_dqkv] (dq|dk|dv). ws: fp32 path only (fer_attention_ws bytes). */
+/* Backward: dqkv [B*N][ld_dqkv] (dq|dk|dv). Optional colsum [3*H*dh] fp32 (+)= column sums of
+ * dqkv over the B*N rows = in_proj.bias gradient, fused into the kernel (per-(batch) partials
+ * + fixed-order reduction). ws >= fer_attention_ws bytes (fp32 path scratch / colsum partials). */
 int fer_attention_bwd(int dtype, const void* qkv, int64_t ld_qkv, const void* out, int64_t ld_out,
                       const void* dout, int64_t ld_dout, const float* lse, void* dqkv, int64_t ld_dqkv, float* ws,
                       int64_t ws_bytes, int B, int N, int H, int dh, float scale, uint32_t drop_thresh,
-                      float drop_scale, uint64_t seed, fer_stream_t stream);
+                      float drop_scale, uint64_t seed, float* colsum, int colsum_accumulate, fer_stream_t stream);
 
 /* Column sums: out[n] (+)= scale * sum_m x[m][n]  (bias gradients). ws >= fer_colsum_ws(M,N). */
 int64_t fer_colsum_ws(int M, int N);

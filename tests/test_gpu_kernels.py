@@ -101,13 +101,15 @@ def test_gemm_epilogue_bias_act_dropout_residual(act):
     # dgrad through dropout + activation derivative (aux), as in the FFN backward
     dy = torch.randn(M, K, generator=g)
     w2 = torch.randn(K, N, generator=g) / math.sqrt(N)  # [out=K, in=N]
-    dF = o.linear_dgrad(bf(dy), bf(w2), dropout=p, seed=seed, drop_ld=N, aux=pre, aux_act=act)
+    cs = torch.zeros(N, device=DEV)  # fused linear1.bias gradient (column sums of dF)
+    dF = o.linear_dgrad(bf(dy), bf(w2), dropout=p, seed=seed, drop_ld=N, aux=pre, aux_act=act, colsum=cs)
     dyr, w2r, hr = bf(dy).float().cpu(), bf(w2).float().cpu(), pre.float().cpu()
     hh = hr.clone().requires_grad_(True)
     aa = torch.nn.functional.gelu(hh) if act == "gelu" else torch.relu(hh)
     dG = dyr @ w2r
     aa.backward(torch.where(keep, dG / (1 - p), torch.zeros(())))
     assert rel_err(dF.cpu(), hh.grad) < 2e-2
+    assert rel_err(cs.cpu(), hh.grad.sum(0)) < 2e-2
 
 
 def test_gemm_keep_rate():
@@ -198,8 +200,10 @@ def test_attention_fwd_bwd(N, H, dh, dtype, p):
     assert (lse.cpu() - lse_ref.reshape(-1)).abs().max().item() < (2e-2 if dtype == "bf16" else 1e-4)
     dd = cast(dout)
     dqkv = torch.empty_like(qd)
-    o.attention_bwd(qd, out, dd, lse, dqkv, B, N, H, dh, dropout=p, seed=seed)
+    cs = torch.full((3 * D,), 0.5, device=DEV)  # fused in_proj.bias gradient, accumulated
+    o.attention_bwd(qd, out, dd, lse, dqkv, B, N, H, dh, dropout=p, seed=seed, colsum=cs, colsum_accumulate=True)
     ref.backward(dd.float().cpu())
+    assert rel_err(cs.cpu() - 0.5, qr.grad.sum(0)) < 2 * tol
     for j, name in enumerate("qkv"):
         a = dqkv.cpu().float()[:, j * D:(j + 1) * D]
         b = qr.grad[:, j * D:(j + 1) * D]
