@@ -129,6 +129,7 @@ template <int NB>
 __global__ __launch_bounds__(64 * NB) __attribute__((amdgpu_waves_per_eu(4))) void attn_fwd_bf16(const bf16* __restrict__ qkv, long ldq, bf16* __restrict__ out,
                                                           long ldo, float* __restrict__ lse, int N, int H, int dh,
                                                           float sl2, uint32_t thr, float dscale, uint64_t seed) {
+  seed = step_seed(seed);
   __shared__ __attribute__((aligned(1024))) char lds[2 * NB * 32 * 128];
   char* Ki = lds;
   char* Vi = lds + NB * 32 * 128;
@@ -201,6 +202,7 @@ __global__ __launch_bounds__(64 * NB) __attribute__((amdgpu_waves_per_eu(4))) vo
                                                          const float* __restrict__ lse, bf16* __restrict__ dqkv,
                                                          long lddq, int N, int H, int dh, float scale, float sl2,
                                                          uint32_t thr, float dscale, uint64_t seed) {
+  seed = step_seed(seed);
   __shared__ __attribute__((aligned(1024))) char lds[2 * NB * 32 * 128];
   char* Ki = lds;
   char* Vi = lds + NB * 32 * 128;
@@ -268,6 +270,7 @@ __global__ __launch_bounds__(64 * NB) void attn_dkv_bf16(const bf16* __restrict_
                                                           const float* __restrict__ lse, bf16* __restrict__ dqkv,
                                                           long lddq, int N, int H, int dh, float scale, float sl2,
                                                           uint32_t thr, float dscale, uint64_t seed) {
+  seed = step_seed(seed);
   constexpr int IMG = NB * 32 * 128;
   __shared__ __attribute__((aligned(1024))) char lds[2 * IMG + 2 * NB * 32 * 4];
   char* Qi = lds;
@@ -434,6 +437,7 @@ __global__ __launch_bounds__(64 * NB) void attn_bwd_fused_bf16(const bf16* __res
                                                                int dh, float scale, float sl2, uint32_t thr,
                                                                float dscale, uint64_t seed, float* __restrict__ cs_part,
                                                                int dbg) {
+  seed = step_seed(seed);
   constexpr int IMG = NB * 32 * 128;
   __shared__ __attribute__((aligned(1024))) char lds[fused_lds_bytes<NB>()];
   char* Qi = lds;
@@ -660,6 +664,7 @@ __global__ void attn_f32_softmax(float* P, float* lse, long rows, int N) {
 }
 __global__ void attn_f32_pv(const float* P, const float* qkv, long ldq, float* out, long ldo, int B, int N, int H,
                             int dh, uint32_t thr, float dscale, uint64_t seed) {
+  seed = step_seed(seed);
   const long idx = blockIdx.x * 256L + threadIdx.x;
   const long total = (long)B * H * N * dh;
   if (idx >= total) return;
@@ -678,6 +683,7 @@ __global__ void attn_f32_pv(const float* P, const float* qkv, long ldq, float* o
 __global__ void attn_f32_ds(const float* P, float* G, const float* qkv, long ldq, const float* out, long ldo,
                             const float* dout, long lddo, int B, int N, int H, int dh, uint32_t thr, float dscale,
                             uint64_t seed) {
+  seed = step_seed(seed);
   const long r = blockIdx.x * 256L + threadIdx.x;
   const long rows = (long)B * H * N;
   if (r >= rows) return;
@@ -697,6 +703,7 @@ __global__ void attn_f32_ds(const float* P, float* G, const float* qkv, long ldq
 __global__ void attn_f32_grads(const float* P, const float* G, const float* qkv, long ldq, const float* dout,
                                long lddo, float* dqkv, long lddq, int B, int N, int H, int dh, float scale,
                                uint32_t thr, float dscale, uint64_t seed) {
+  seed = step_seed(seed);
   const long idx = blockIdx.x * 256L + threadIdx.x;
   const long total = (long)B * H * N * dh;
   if (idx >= total) return;
@@ -731,6 +738,8 @@ __global__ void attn_f32_grads(const float* P, const float* G, const float* qkv,
 }  // namespace fer
 
 using namespace fer;
+
+int fer::set_step_ptr_attention(const uint64_t* p) { return set_step_ptr_here(p) == hipSuccess ? 0 : -1; }
 
 extern "C" int64_t fer_attention_ws(int dtype, int B, int N, int H) {
   // fp32 path: P and dS slabs, then the stand-alone colsum pass's partials; bf16: the fused

@@ -32,3 +32,11 @@ extern "C" int fer_gemm(const fer_gemm_desc* d, const fer_epilogue* e, fer_strea
   if (!d || !e) return fer::set_error("gemm: null descriptor");
   return fer::gemm_launch(*d, *e, (hipStream_t)stream);
 }
+
+extern "C" int fer_set_step_counter(const uint64_t* counter) {
+  // every code object that has dropout kernels keeps its own copy of the pointer
+  if (fer::set_step_ptr_gemm(counter) || fer::set_step_ptr_attention(counter) ||
+      fer::set_step_ptr_layernorm(counter) || fer::set_step_ptr_misc(counter))
+    return fer::set_error("set_step_counter: hipMemcpyToSymbol failed");
+  return 0;
+}

@@ -98,6 +98,22 @@ FER_DEV uint32_t fer_hash(uint64_t seed, uint32_t pair) {
   x ^= x >> 16;
   return x;
 }
+// Device-side step counter for graph-replayed training steps (fer_set_step_counter): a
+// captured launch keeps its host seed, so every dropout kernel mixes the current step into it.
+// One pointer per code object (each .hip file is its own code object); null = no counter.
+static __device__ const uint64_t* fer_step_ptr = nullptr;
+FER_DEV uint64_t step_seed(uint64_t seed) {
+  const uint64_t* p = fer_step_ptr;
+  if (!p) return seed;
+  uint64_t z = seed ^ (*p * 0x9E3779B97F4A7C15ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+// host side, per code object
+static inline hipError_t set_step_ptr_here(const uint64_t* p) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(fer_step_ptr), &p, sizeof(p));
+}
 FER_DEV bool drop_keep(uint64_t seed, uint32_t idx, uint32_t thresh) {
   if (thresh == 0u) return true;
   const uint32_t h = fer_hash(seed, idx >> 1);

@@ -24,6 +24,11 @@ struct GemmArgs {
 };
 
 int set_error(const char* msg);
+// per-code-object setters of the device step-counter pointer (common.h step_seed)
+int set_step_ptr_gemm(const uint64_t* p);
+int set_step_ptr_attention(const uint64_t* p);
+int set_step_ptr_layernorm(const uint64_t* p);
+int set_step_ptr_misc(const uint64_t* p);
 int hip_check(const char* what);
 int gemm_launch(const GemmDesc& d, const EpiArgs& e, hipStream_t st);
 inline int ceil_div(long a, long b);

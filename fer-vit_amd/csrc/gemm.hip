@@ -41,7 +41,7 @@ FER_DEV bf16x8 pack8(f32x4 a, f32x4 b) {
   return bf16x8{(bf16)a[0], (bf16)a[1], (bf16)a[2], (bf16)a[3], (bf16)b[0], (bf16)b[1], (bf16)b[2], (bf16)b[3]};
 }
 FER_DEV void epi8_bf16(const EpiArgs& e, long m, long n, f32x4& v0, f32x4& v1, f32x4 b0, f32x4 b1, bf16x8 x,
-                       float ps) {
+                       float ps, uint64_t seed) {
   v0 = v0 * e.alpha + b0;
   v1 = v1 * e.alpha + b1;
   if (e.pre) *(bf16x8*)((bf16*)e.pre + m * e.ldp + n) = pack8(v0, v1);
@@ -60,8 +60,8 @@ FER_DEV void epi8_bf16(const EpiArgs& e, long m, long n, f32x4& v0, f32x4& v1, f
   }
   if (e.drop_thresh) {
     const uint32_t idx = (uint32_t)m * (uint32_t)e.drop_ld + (uint32_t)n;
-    drop4(e.seed, idx, e.drop_thresh, e.drop_scale, v0);
-    drop4(e.seed, idx + 4, e.drop_thresh, e.drop_scale, v1);
+    drop4(seed, idx, e.drop_thresh, e.drop_scale, v0);
+    drop4(seed, idx + 4, e.drop_thresh, e.drop_scale, v1);
   }
   if (e.post_scale) {
     v0 *= ps;
@@ -100,7 +100,7 @@ FER_DEV void epi8_bf16(const EpiArgs& e, long m, long n, f32x4& v0, f32x4& v1, f
 }
 
 template <typename T>
-FER_DEV void epi4(const EpiArgs& e, long m, long n, f32x4 v) {
+FER_DEV void epi4(const EpiArgs& e, long m, long n, f32x4 v, uint64_t seed) {
   v *= e.alpha;
   if (e.bias) v += *(const f32x4*)(e.bias + n);
   if (e.pre) store4<T>((T*)e.pre + m * e.ldp + n, v);
@@ -108,7 +108,7 @@ FER_DEV void epi4(const EpiArgs& e, long m, long n, f32x4 v) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) v[r] = act_fwd(e.act, v[r]);
   }
-  if (e.drop_thresh) drop4(e.seed, (uint32_t)m * (uint32_t)e.drop_ld + (uint32_t)n, e.drop_thresh, e.drop_scale, v);
+  if (e.drop_thresh) drop4(seed, (uint32_t)m * (uint32_t)e.drop_ld + (uint32_t)n, e.drop_thresh, e.drop_scale, v);
   if (e.post_scale) v *= *e.post_scale;
   if (e.aux) {
     f32x4 a = load4<T>((const T*)e.aux + m * e.ldx + n);
@@ -320,6 +320,7 @@ FER_DEV void tile_epilogue(const GemmArgs& g, const EpiArgs& e, AccT (&acc)[FN][
     b1 = *(const f32x4*)(e.bias + n + 4);
   }
   const float ps = e.post_scale ? *e.post_scale : 1.f;
+  const uint64_t seed = e.drop_thresh ? step_seed(e.seed) : 0;
   const void* xs = e.res ? e.res : e.aux;  // the row operand brought in by DMA
   const long ldxs = e.res ? e.ldr : e.ldx;
   const __amdgpu_buffer_rsrc_t rx = make_rsrc(xs);
@@ -382,7 +383,7 @@ FER_DEV void tile_epilogue(const GemmArgs& g, const EpiArgs& e, AccT (&acc)[FN][
       f32x4 v0 = *(const f32x4*)(stg + swz(r, tc)), v1 = *(const f32x4*)(stg + swz(r, tc + 4));
       const bf16x8 x = xs ? *(const bf16x8*)(xh + (r * BN + tc) * 2) : bf16x8{};
       if (nok && m < g.M) {
-        epi8_bf16(e, m, n, v0, v1, b0, b1, x, ps);
+        epi8_bf16(e, m, n, v0, v1, b0, b1, x, ps, seed);
         cs0 += v0;
         cs1 += v1;
       }
@@ -821,11 +822,12 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
                                                            EpiArgs e) {
   const long n4 = N >> 2;
   const long total = M * n4;
+  const uint64_t seed = e.drop_thresh ? step_seed(e.seed) : 0;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256L) {
     const long m = i / n4, n = (i - m * n4) * 4;
     f32x4 v = *(const f32x4*)(ws + m * N + n);
     for (int s = 1; s < splits; ++s) v += *(const f32x4*)(ws + (long)s * M * N + m * N + n);
-    epi4<T>(e, m, n, v);
+    epi4<T>(e, m, n, v, seed);
   }
 }
 
@@ -840,6 +842,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs g, EpiArgs e, in
   const float* B = (const float*)g.B;
   float acc[4][4] = {};
   const int ty = t >> 4, tx = t & 15;
+  const uint64_t seed = e.drop_thresh ? step_seed(e.seed) : 0;
   for (int k0 = 0; k0 < g.K; k0 += 16) {
     for (int i = t; i < 16 * 64; i += 256) {
       int kk, mm;
@@ -867,7 +870,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs g, EpiArgs e, in
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const long m = m0 + ty * 4 + r, n = n0 + tx * 4;
-    if (m < g.M && n < g.N) epi4<float>(e, m, n, f32x4{acc[r][0], acc[r][1], acc[r][2], acc[r][3]});
+    if (m < g.M && n < g.N) epi4<float>(e, m, n, f32x4{acc[r][0], acc[r][1], acc[r][2], acc[r][3]}, seed);
   }
 }
 
@@ -1011,6 +1014,8 @@ int gemm_launch(const GemmDesc& d, const EpiArgs& e_in, hipStream_t st) {
 }
 
 }  // namespace fer
+
+int fer::set_step_ptr_gemm(const uint64_t* p) { return set_step_ptr_here(p) == hipSuccess ? 0 : -1; }
 
 extern "C" int64_t fer_gemm_colsum_ws(int M, int N) {
   // tile partials (128-row tiles at most) or the stand-alone colsum pass's partials

@@ -65,6 +65,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, l
                                                      T* __restrict__ dx, long lddx, T* __restrict__ dxd,
                                                      uint32_t thr, float dscale, uint64_t seed,
                                                      float* __restrict__ part, int want_part, int M, int D) {
+  seed = step_seed(seed);
   __shared__ float red[4][LN_VPL * 256];  // one partial at a time: 16 KB keeps 4+ blocks/CU
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int nv = D >> 2;
@@ -166,6 +167,8 @@ static int ln_bwd_blocks(int M) { return std::max(1, std::min(ceil_div(M, 16), 1
 }  // namespace fer
 
 using namespace fer;
+
+int fer::set_step_ptr_layernorm(const uint64_t* p) { return set_step_ptr_here(p) == hipSuccess ? 0 : -1; }
 
 extern "C" int fer_layernorm_fwd(int dtype, const void* x, int64_t ldx, const float* gamma, const float* beta,
                                  int gamma_rows, int row_div, void* y, int64_t ldy, float* mean, float* rstd, int M,

@@ -96,6 +96,7 @@ template <typename T>
 __global__ __launch_bounds__(256) void tokens_fwd_kernel(const T* __restrict__ emb, const float* __restrict__ cls,
                                                          const float* __restrict__ pos, T* __restrict__ t, int B,
                                                          int n, int D, uint32_t thr, float dscale, uint64_t seed) {
+  seed = step_seed(seed);
   const int N = n + 1;
   const long total = (long)B * N * D;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256L) {
@@ -113,6 +114,7 @@ template <typename T>
 __global__ __launch_bounds__(256) void tokens_bwd_kernel(const T* __restrict__ dt, T* __restrict__ demb, int B, int n,
                                                          int D, uint32_t thr, float dscale, uint64_t seed,
                                                          float* __restrict__ part, int bchunk) {
+  seed = step_seed(seed);
   const int N = n + 1;
   const long cols = (long)N * D;
   const long j = blockIdx.x * 256L + threadIdx.x;  // (token, d)
@@ -147,6 +149,7 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(const T* __restrict__ t, 
                                                        const float* __restrict__ W, const float* __restrict__ bias,
                                                        float* __restrict__ logits, float* __restrict__ stats, int D,
                                                        int C, uint32_t thr, float dscale, uint64_t seed) {
+  seed = step_seed(seed);
   __shared__ float h[1024];
   __shared__ float red[8];
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -193,6 +196,7 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const T* __restrict__ t, 
                                                        const float* __restrict__ dlogits, T* __restrict__ dt, int D,
                                                        int C, uint32_t thr, float dscale, uint64_t seed,
                                                        float* __restrict__ part) {
+  seed = step_seed(seed);
   __shared__ float xh[1024], gh[1024];
   __shared__ float red[8];
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -579,6 +583,7 @@ __global__ void sum_final_kernel(const float* __restrict__ part, int n, float* o
 template <typename T>
 __global__ void dropout_kernel(const T* __restrict__ x, T* __restrict__ y, long n, uint32_t thr, float sc,
                                uint64_t seed) {
+  seed = step_seed(seed);
   for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256L)
     y[i] = from_f<T>(drop_keep(seed, (uint32_t)i, thr) ? to_f<T>(x[i]) * sc : 0.f);
 }
@@ -592,11 +597,13 @@ __global__ void clip_coef_kernel(const float* sumsq, float sq_scale, float max_n
 __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                     float* __restrict__ m, float* __restrict__ v, bf16* __restrict__ pb,
                                                     const fer_adamw_segment* __restrict__ segs, float gscale,
-                                                    const float* __restrict__ clip) {
+                                                    const float* __restrict__ clip,
+                                                    const uint64_t* __restrict__ step_add) {
   const fer_adamw_segment sg = segs[blockIdx.y];
   const float sc = gscale * (clip ? *clip : 1.f);
-  const float bc1 = 1.f - powf(sg.beta1, (float)sg.step);
-  const float bc2 = 1.f - powf(sg.beta2, (float)sg.step);
+  const float t = (float)(sg.step + (step_add ? (long)*step_add : 0L));  // + graph replays
+  const float bc1 = 1.f - powf(sg.beta1, t);
+  const float bc2 = 1.f - powf(sg.beta2, t);
   const float step_size = sg.lr / bc1;
   const float bc2s = sqrtf(bc2);
   const float decay = 1.f - sg.lr * sg.weight_decay;
@@ -619,6 +626,8 @@ static int grid_for(long n) { return (int)std::max<long>(1, std::min<long>((n + 
 }  // namespace fer
 
 using namespace fer;
+
+int fer::set_step_ptr_misc(const uint64_t* p) { return set_step_ptr_here(p) == hipSuccess ? 0 : -1; }
 
 extern "C" int64_t fer_colsum_ws(int M, int N) { return (int64_t)colsum_nblk(M) * N * 4; }
 
@@ -853,12 +862,21 @@ extern "C" int fer_dropout(int dtype, const void* x, void* y, int64_t n, uint32_
                        (long)n, drop_thresh, drop_scale, seed);
   return hip_check("dropout");
 }
+__global__ void step_advance_kernel(uint64_t* counter) {
+  if (threadIdx.x == 0) *counter += 1;
+}
+
+extern "C" int fer_step_advance(uint64_t* counter, fer_stream_t stream) {
+  hipLaunchKernelGGL(step_advance_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, counter);
+  return hip_check("step_advance");
+}
+
 extern "C" int fer_adamw(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, void* param_bf16,
                          const fer_adamw_segment* segs_device, int nsegs, int64_t max_seg_numel, float grad_scale,
-                         const float* clip_coef, fer_stream_t stream) {
+                         const float* clip_coef, const uint64_t* step_add, fer_stream_t stream) {
   if (nsegs <= 0) return 0;
   dim3 grid((unsigned)std::max<long>(1, std::min<long>((max_seg_numel + 255) / 256, 1024)), nsegs);
   hipLaunchKernelGGL(adamw_kernel, grid, dim3(256), 0, (hipStream_t)stream, param, grad, exp_avg, exp_avg_sq,
-                     (bf16*)param_bf16, segs_device, grad_scale, clip_coef);
+                     (bf16*)param_bf16, segs_device, grad_scale, clip_coef, step_add);
   return hip_check("adamw");
 }

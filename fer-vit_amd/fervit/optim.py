@@ -27,6 +27,8 @@ class FusedAdamW(torch.optim.Optimizer):
         self._seg_key = None
         self.grad_scale = 1.0        # e.g. 1/world after an all-reduce sum
         self.clip_coef: Optional[torch.Tensor] = None  # device scalar, consumed by the next step
+        self._step_counter: Optional[torch.Tensor] = None  # graph mode (freeze_for_graph)
+        self._frozen = None
 
     def _bind(self):
         flat = self.model.fer_flat() if self.model is not None else None
@@ -38,10 +40,16 @@ class FusedAdamW(torch.optim.Optimizer):
             self._v = torch.zeros_like(flat.data)
         return flat
 
-    @torch.no_grad()
-    def step(self, closure=None):
-        loss = closure() if closure is not None else None
+    def freeze_for_graph(self, counter: torch.Tensor) -> None:
+        """Graph mode (fervit.graph.StepGraph): the segment table is uploaded once and the
+        AdamW step of every parameter becomes (its host step count now) + *counter, the device
+        step counter the captured step advances. Call after the eager warm-up steps."""
         flat = self._bind()
+        segs, maxn = self._segments(flat, bump=False)
+        self._frozen = (self._upload(segs, flat), len(segs), maxn)
+        self._step_counter = counter
+
+    def _segments(self, flat, bump: bool):
         segs = []
         maxn = 0
         for g in self.param_groups:
@@ -50,23 +58,46 @@ class FusedAdamW(torch.optim.Optimizer):
                 if p.grad is None:
                     continue
                 st = self.state[p]
-                st["step"] = st.get("step", 0) + 1
+                if bump:
+                    st["step"] = st.get("step", 0) + 1
                 n = p.numel()
                 maxn = max(maxn, n)
-                segs.append((flat.offsets[id(p)], n, g["lr"], g["weight_decay"], b1, b2, g["eps"], st["step"]))
+                segs.append((flat.offsets[id(p)], n, g["lr"], g["weight_decay"], b1, b2, g["eps"],
+                             st.get("step", 0)))
                 if p.grad.data_ptr() != flat.grad_views[id(p)].data_ptr():
                     flat.grad_views[id(p)].copy_(p.grad)
-        if not segs:
-            return loss
+        return segs, maxn
+
+    @staticmethod
+    def _upload(segs, flat):
         arr = (AdamWSegment * len(segs))(*[AdamWSegment(*s) for s in segs])
         host = torch.frombuffer(bytearray(ctypes.string_at(ctypes.addressof(arr), ctypes.sizeof(arr))),
                                 dtype=torch.uint8)
-        dev = host.to(flat.data.device, non_blocking=False)
+        return host.to(flat.data.device, non_blocking=False)
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = closure() if closure is not None else None
+        flat = self._bind()
+        if self._frozen is not None:  # graph mode: static segments, device step counter
+            dev, nseg, maxn = self._frozen
+            half = flat.bf16()
+            check(lib().fer_adamw(flat.data.data_ptr(), flat.grad.data_ptr(), self._m.data_ptr(),
+                                  self._v.data_ptr(), half.data_ptr(), dev.data_ptr(), nseg, maxn,
+                                  float(self.grad_scale), ops.ptr(self.clip_coef),
+                                  self._step_counter.data_ptr(), ops.stream()), "adamw")
+            flat.mark_half_fresh()
+            self.clip_coef = None
+            return loss
+        segs, maxn = self._segments(flat, bump=True)
+        if not segs:
+            return loss
+        dev = self._upload(segs, flat)
         self._segs_dev = dev
         half = flat.bf16()
         check(lib().fer_adamw(flat.data.data_ptr(), flat.grad.data_ptr(), self._m.data_ptr(), self._v.data_ptr(),
                               half.data_ptr(), dev.data_ptr(), len(segs), maxn, float(self.grad_scale),
-                              ops.ptr(self.clip_coef), ops.stream()), "adamw")
+                              ops.ptr(self.clip_coef), None, ops.stream()), "adamw")
         flat.mark_half_fresh()
         self.clip_coef = None
         return loss

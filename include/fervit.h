@@ -197,7 +197,16 @@ typedef struct {
 } fer_adamw_segment;
 int fer_adamw(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, void* param_bf16,
               const fer_adamw_segment* segs_device, int nsegs, int64_t max_seg_numel, float grad_scale,
-              const float* clip_coef, fer_stream_t stream);
+              const float* clip_coef, const uint64_t* step_add, fer_stream_t stream);
+
+/* Graph-replayed training steps (hipGraph capture of a whole step; no reference counterpart,
+ * the reference trains eagerly). counter: caller-owned device uint64. After
+ * fer_set_step_counter(counter) every dropout kernel mixes *counter into its seed, so a replayed
+ * launch with a captured (constant) seed still draws a fresh mask each step; fer_adamw adds
+ * *step_add to each segment's step. fer_step_advance(counter) (+1, a 1-thread kernel) is the
+ * first node of the captured step. NULL disables (default). */
+int fer_set_step_counter(const uint64_t* counter);
+int fer_step_advance(uint64_t* counter, fer_stream_t stream);
 /* sum of squares of grad (for clip_grad_norm_), out fp32 scalar; ws >= fer_colsum_ws(1, 4096). */
 int fer_sumsq(const float* x, int64_t n, float* out, float* ws, int64_t ws_bytes, fer_stream_t stream);
 /* clip coefficient: coef = min(1, max_norm / (sqrt(sumsq*sq_scale) + 1e-6)) (torch clip_grad_norm_). */
