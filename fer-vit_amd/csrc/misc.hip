@@ -862,6 +862,42 @@ extern "C" int fer_dropout(int dtype, const void* x, void* y, int64_t n, uint32_
                        (long)n, drop_thresh, drop_scale, seed);
   return hip_check("dropout");
 }
+// ------------------------------------------------------------------ latent augmentation
+// LatentAugment (`data/latent_dataset.py:6-49`) on device, in the reference's order:
+// x += N(0, noise_std) (Box-Muller on two 32-bit hashes), x *= U(scale_lo, scale_hi) drawn once
+// per sample, x *= (U(0,1) > mask_prob). Same distributions as the reference's torch RNG calls
+// (not the same stream). Counter-based like the dropout masks: element i of the batch.
+FER_DEV float u01(uint32_t h) { return ((float)(h >> 8) + 0.5f) * (1.f / 16777216.f); }
+__global__ void latent_augment_kernel(float* __restrict__ x, long n, int LD, float noise_std, float scale_lo,
+                                      float scale_hi, float mask_prob, uint64_t seed) {
+  seed = step_seed(seed);
+  const uint64_t s_noise = seed, s_scale = seed ^ 0x5851F42D4C957F2Dull, s_mask = seed ^ 0x14057B7EF767814Full;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256L) {
+    float v = x[i];
+    if (noise_std > 0.f) {
+      const uint32_t e = (uint32_t)i;
+      const float u1 = u01(fer_hash(s_noise, 2u * e)), u2 = u01(fer_hash(s_noise, 2u * e + 1u));
+      v += noise_std * sqrtf(-2.f * logf(u1)) * cosf(6.28318530717958648f * u2);
+    }
+    if (scale_hi > scale_lo || scale_lo != 1.f) {
+      const uint32_t b = (uint32_t)(i / LD);
+      v *= scale_lo + (scale_hi - scale_lo) * u01(fer_hash(s_scale, b));
+    }
+    if (mask_prob > 0.f && !(u01(fer_hash(s_mask, (uint32_t)i)) > mask_prob)) v = 0.f;
+    x[i] = v;
+  }
+}
+
+extern "C" int fer_latent_augment(float* x, int64_t B, int LD, float noise_std, float scale_lo, float scale_hi,
+                                  float mask_prob, uint64_t seed, fer_stream_t stream) {
+  const long n = (long)B * LD;
+  if (n <= 0) return 0;
+  if (n > 0x7FFFFFFFL) return set_error("latent_augment: more than 2^31 elements per call");
+  hipLaunchKernelGGL(latent_augment_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, x, n, LD,
+                     noise_std, scale_lo, scale_hi, mask_prob, seed);
+  return hip_check("latent_augment");
+}
+
 __global__ void step_advance_kernel(uint64_t* counter) {
   if (threadIdx.x == 0) *counter += 1;
 }

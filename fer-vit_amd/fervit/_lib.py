@@ -74,6 +74,7 @@ SIGNATURES = {
     "fer_dropout": (i32, [i32, vp, vp, i64, u32, f32, u64, vp]),
     "fer_adamw": (i32, [fp, fp, fp, fp, vp, vp, i32, i64, f32, fp, vp, vp]),
     "fer_set_step_counter": (i32, [vp]),
+    "fer_latent_augment": (i32, [fp, i64, i32, f32, f32, f32, f32, u64, vp]),
     "fer_step_advance": (i32, [vp, vp]),
     "fer_sumsq": (i32, [fp, i64, fp, fp, i64, vp]),
     "fer_clip_coef": (i32, [fp, f32, f32, fp, vp]),

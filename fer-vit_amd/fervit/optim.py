@@ -40,6 +40,54 @@ class FusedAdamW(torch.optim.Optimizer):
             self._v = torch.zeros_like(flat.data)
         return flat
 
+    # ---- torch.optim.AdamW-format state (checkpoints: utils/experiment_logger.py:121-145)
+    def state_dict(self):
+        """torch.optim.AdamW layout: per-parameter {'step', 'exp_avg', 'exp_avg_sq'} (moments
+        copied out of the flat buffers) and the AdamW param-group keys, so a checkpoint written
+        here resumes under torch.optim.AdamW and vice versa."""
+        if self._flat is not None and self._m is not None:
+            flat = self._flat
+            for g in self.param_groups:
+                for p in g["params"]:
+                    st = self.state.get(p)
+                    if st is None or id(p) not in flat.offsets:
+                        continue
+                    st["exp_avg"] = flat.view(p, self._m).detach().clone()
+                    st["exp_avg_sq"] = flat.view(p, self._v).detach().clone()
+        sd = super().state_dict()
+        sd["state"] = {k: dict(v) for k, v in sd["state"].items()}  # detach from the live state
+        sd["param_groups"] = [dict(g) for g in sd["param_groups"]]
+        for st in sd["state"].values():
+            if not torch.is_tensor(st.get("step", 0)):
+                st["step"] = torch.tensor(float(st.get("step", 0)))
+        for g in sd["param_groups"]:
+            for k, v in (("amsgrad", False), ("maximize", False), ("foreach", None), ("capturable", False),
+                         ("differentiable", False), ("fused", None)):
+                g.setdefault(k, v)
+        for g in self.param_groups:  # the live state keeps only the host step count
+            for p in g["params"]:
+                st = self.state.get(p)
+                if st is not None:
+                    st.pop("exp_avg", None)
+                    st.pop("exp_avg_sq", None)
+        return sd
+
+    def load_state_dict(self, state_dict):
+        super().load_state_dict(state_dict)
+        flat = self._bind()
+        with torch.no_grad():
+            for g in self.param_groups:
+                for p in g["params"]:
+                    st = self.state.get(p)
+                    if not st:
+                        continue
+                    if "exp_avg" in st:
+                        flat.view(p, self._m).copy_(st.pop("exp_avg"))
+                    if "exp_avg_sq" in st:
+                        flat.view(p, self._v).copy_(st.pop("exp_avg_sq"))
+                    if torch.is_tensor(st.get("step")):
+                        st["step"] = int(st["step"].item())
+
     def freeze_for_graph(self, counter: torch.Tensor) -> None:
         """Graph mode (fervit.graph.StepGraph): the segment table is uploaded once and the
         AdamW step of every parameter becomes (its host step count now) + *counter, the device

@@ -199,6 +199,12 @@ int fer_adamw(float* param, const float* grad, float* exp_avg, float* exp_avg_sq
               const fer_adamw_segment* segs_device, int nsegs, int64_t max_seg_numel, float grad_scale,
               const float* clip_coef, const uint64_t* step_add, fer_stream_t stream);
 
+/* LatentAugment (`data/latent_dataset.py:6-49`) on a device batch x fp32 [B][LD], in place:
+ * x += N(0, noise_std); x *= U(scale_lo, scale_hi) per sample; x *= (U(0,1) > mask_prob).
+ * Counter-based draws keyed by seed (and the step counter below, when set). */
+int fer_latent_augment(float* x, int64_t B, int LD, float noise_std, float scale_lo, float scale_hi,
+                       float mask_prob, uint64_t seed, fer_stream_t stream);
+
 /* Graph-replayed training steps (hipGraph capture of a whole step; no reference counterpart,
  * the reference trains eagerly). counter: caller-owned device uint64. After
  * fer_set_step_counter(counter) every dropout kernel mixes *counter into its seed, so a replayed
