@@ -38,6 +38,11 @@ class AdamWSegment(C.Structure):
                 ("beta2", f32), ("eps", f32), ("step", i32)]
 
 
+class ImageAug(C.Structure):
+    _fields_ = [("flip_p", f32), ("degrees", f32), ("brightness", f32), ("contrast", f32), ("saturation", f32),
+                ("hue", f32), ("translate", f32), ("scale_lo", f32), ("scale_hi", f32)]
+
+
 # name -> (restype, argtypes)
 SIGNATURES = {
     "fer_gemm": (i32, [C.POINTER(GemmDesc), C.POINTER(Epilogue), vp]),
@@ -76,6 +81,8 @@ SIGNATURES = {
     "fer_set_step_counter": (i32, [vp]),
     "fer_latent_augment": (i32, [fp, i64, i32, f32, f32, f32, f32, u64, vp]),
     "fer_step_advance": (i32, [vp, vp]),
+    "fer_image_aug_draw": (i32, [fp, i32, i32, vp, u64, vp]),
+    "fer_image_augment": (i32, [vp, vp, vp, i32, i32, fp, i32, vp, vp, fp, vp]),
     "fer_sumsq": (i32, [fp, i64, fp, fp, i64, vp]),
     "fer_clip_coef": (i32, [fp, f32, f32, fp, vp]),
     "fer_last_error": (C.c_char_p, []),

@@ -205,6 +205,26 @@ int fer_adamw(float* param, const float* grad, float* exp_avg, float* exp_avg_sq
 int fer_latent_augment(float* x, int64_t B, int LD, float noise_std, float scale_lo, float scale_hi,
                        float mask_prob, uint64_t seed, fer_stream_t stream);
 
+/* ImageViT input transforms (`data/image_dataset.py:139-173`, torchvision on PIL images) on the
+ * device, SURVEY §8(f) row 4. Sources: B decoded uint8 HWC images (C = 1 or 3) packed in one
+ * device buffer, image b at src + offsets[b], hwc[3b..3b+2] = H, W, C. Output fp32 NCHW
+ * [B][3][S][S] normalised with mean3/std3 (host arrays).
+ *   train = 0: Resize((S,S)) -> ToTensor -> Normalize (get_val_transforms)
+ *   train = 1: Resize -> HorizontalFlip -> Rotation -> ColorJitter -> Affine -> ... (get_train_transforms)
+ * with per-image parameter records params[B][16] (fer_image_aug_draw, or given by the caller):
+ * [0] flip, [1] angle deg, [2..5] brightness/contrast/saturation/hue factors, [6..9] jitter op
+ * order (0 b, 1 c, 2 s, 3 h), [10] tx, [11] ty (pixels), [12] scale, [13] hue enabled.
+ * Every stage follows PIL's own arithmetic (fixed-point resampling and rotation, uint8 blends,
+ * 8-bit HSV), so the output equals the reference pipeline's for the same parameters.
+ * S <= 1024; any source size (shrinking widens the resize filter, as in PIL). */
+typedef struct {
+  float flip_p, degrees, brightness, contrast, saturation, hue, translate, scale_lo, scale_hi;
+} fer_image_aug;
+int fer_image_aug_draw(float* params, int B, int S, const fer_image_aug* aug, uint64_t seed, fer_stream_t stream);
+int fer_image_augment(const uint8_t* src, const int64_t* offsets, const int32_t* hwc, int B, int S,
+                      const float* params, int train, const float* mean3, const float* std3, float* out,
+                      fer_stream_t stream);
+
 /* Graph-replayed training steps (hipGraph capture of a whole step; no reference counterpart,
  * the reference trains eagerly). counter: caller-owned device uint64. After
  * fer_set_step_counter(counter) every dropout kernel mixes *counter into its seed, so a replayed
