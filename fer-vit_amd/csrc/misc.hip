@@ -623,6 +623,58 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const
 
 static int grid_for(long n) { return (int)std::max<long>(1, std::min<long>((n + 255) / 256, 8192)); }
 
+// Transposed bf16 weight shadow: for each 2-D segment {off, rows, cols, first_tile} of a flat
+// buffer, dst[off + c*rows + r] = src[off + r*cols + c]. One launch over all segments (64x64
+// tiles through LDS, block -> segment by binary search on first_tile). The dgrad GEMMs read the
+// result as a K-contiguous operand (dX = dY W = dY (W^T)^T), which streams through the
+// 16-byte-row DMA path instead of the transposed-LDS-read path of an MN operand.
+__global__ __launch_bounds__(256) void transpose_segs_kernel(const uint16_t* __restrict__ src,
+                                                             uint16_t* __restrict__ dst,
+                                                             const int64_t* __restrict__ segs, int nseg) {
+  __shared__ uint32_t tile[64][33];  // 64 rows x 64 bf16 (as 32 pairs), +1 word pad
+  const long t = blockIdx.x;
+  int lo = 0, hi = nseg - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (segs[mid * 4 + 3] <= t) lo = mid;
+    else hi = mid - 1;
+  }
+  const long off = segs[lo * 4], rows = segs[lo * 4 + 1], cols = segs[lo * 4 + 2];
+  const long lt = t - segs[lo * 4 + 3], tc = (cols + 63) / 64;
+  const long r0 = (lt / tc) * 64, c0 = (lt % tc) * 64;
+  const uint16_t* s = src + off;
+  uint16_t* d = dst + off;
+  const int tid = threadIdx.x;
+  // load: row r, column pair cp (2 bf16); 64 x 32 pairs = 2048 / 256 threads
+  for (int i = tid; i < 64 * 32; i += 256) {
+    const int r = i >> 5, cp = i & 31;
+    const long gr = r0 + r, gc = c0 + cp * 2;
+    uint32_t v = 0;
+    if (gr < rows) {
+      const uint16_t lo16 = gc < cols ? s[gr * cols + gc] : 0;
+      const uint16_t hi16 = gc + 1 < cols ? s[gr * cols + gc + 1] : 0;
+      v = lo16 | ((uint32_t)hi16 << 16);
+    }
+    tile[r][cp] = v;
+  }
+  __syncthreads();
+  // store: output row c (= input column), pair of input rows rp
+  for (int i = tid; i < 64 * 32; i += 256) {
+    const int c = i >> 5, rp = i & 31;
+    const long gc = c0 + c, gr = r0 + rp * 2;
+    if (gc >= cols) continue;
+    const uint32_t a = tile[rp * 2][c >> 1], b = tile[rp * 2 + 1][c >> 1];
+    const uint16_t x0 = (c & 1) ? (uint16_t)(a >> 16) : (uint16_t)a;
+    const uint16_t x1 = (c & 1) ? (uint16_t)(b >> 16) : (uint16_t)b;
+    if (gr + 1 < rows && ((off + gc * rows + gr) & 1) == 0) {
+      *(uint32_t*)(d + gc * rows + gr) = x0 | ((uint32_t)x1 << 16);
+    } else {
+      if (gr < rows) d[gc * rows + gr] = x0;
+      if (gr + 1 < rows) d[gc * rows + gr + 1] = x1;
+    }
+  }
+}
+
 }  // namespace fer
 
 using namespace fer;
@@ -886,6 +938,15 @@ __global__ void latent_augment_kernel(float* __restrict__ x, long n, int LD, flo
     if (mask_prob > 0.f && !(u01(fer_hash(s_mask, (uint32_t)i)) > mask_prob)) v = 0.f;
     x[i] = v;
   }
+}
+
+extern "C" int fer_transpose_bf16_segments(const void* src, void* dst, const int64_t* segs, int nseg,
+                                          int64_t total_tiles, fer_stream_t stream) {
+  if (nseg <= 0 || total_tiles <= 0) return 0;
+  if (!src || !dst || !segs || src == dst) return set_error("transpose_bf16_segments: bad pointers (in-place is not supported)");
+  hipLaunchKernelGGL(transpose_segs_kernel, dim3((unsigned)total_tiles), dim3(256), 0, (hipStream_t)stream,
+                     (const uint16_t*)src, (uint16_t*)dst, segs, nseg);
+  return hip_check("transpose_bf16_segments");
 }
 
 extern "C" int fer_latent_augment(float* x, int64_t B, int LD, float noise_std, float scale_lo, float scale_hi,

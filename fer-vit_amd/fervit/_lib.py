@@ -81,6 +81,7 @@ SIGNATURES = {
     "fer_set_step_counter": (i32, [vp]),
     "fer_latent_augment": (i32, [fp, i64, i32, f32, f32, f32, f32, u64, vp]),
     "fer_step_advance": (i32, [vp, vp]),
+    "fer_transpose_bf16_segments": (i32, [vp, vp, vp, i32, i64, vp]),
     "fer_image_aug_draw": (i32, [fp, i32, i32, vp, u64, vp]),
     "fer_image_augment": (i32, [vp, vp, vp, i32, i32, fp, i32, vp, vp, fp, vp]),
     "fer_sumsq": (i32, [fp, i64, fp, fp, i64, vp]),

@@ -72,6 +72,9 @@ class FlatParams:
         self.grad = torch.zeros(self.numel, dtype=torch.float32, device=dev)
         self.half: Optional[torch.Tensor] = None
         self.half_version = -1
+        self.half_t: Optional[torch.Tensor] = None  # transposed bf16 copies of the 2-D params
+        self._tsegs: Optional[torch.Tensor] = None
+        self._ttiles = 0
         with torch.no_grad():
             for p in self.params:
                 v = self.view(p)
@@ -99,6 +102,7 @@ class FlatParams:
         if v != self.half_version:
             ops.cast_bf16(self.data, self.half)
             self.half_version = v
+            self.refresh_half_t()
         return self.half
 
     def version(self) -> int:
@@ -107,11 +111,46 @@ class FlatParams:
         return self.data._version + sum(p._version for p in self.params)
 
     def mark_half_fresh(self):
-        """Called by the fused optimizer, which refreshes the bf16 copy itself."""
+        """Called by the fused optimizer right after it rewrote the bf16 copy (same stream):
+        the transposed copies follow in the same stream order (and the same captured graph)."""
         self.half_version = self.version()
+        self.refresh_half_t()
 
     def half_view(self, p):
         return self.view(p, self.bf16())
+
+    # ---- transposed bf16 copies (dgrad operands, K-contiguous)
+    def refresh_half_t(self):
+        if self.half_t is None or self.half is None:
+            return
+        from ._lib import check, lib
+        from . import ops
+
+        check(lib().fer_transpose_bf16_segments(self.half.data_ptr(), self.half_t.data_ptr(), self._tsegs.data_ptr(),
+                                                self._tsegs.shape[0], self._ttiles, ops.stream()), "transpose")
+
+    def half_t_view(self, p):
+        """bf16 W^T ([cols][rows]) of a 2-D parameter, kept in step with the bf16 shadow: one
+        batched transpose launch per refresh of the shadow (optimizer step or cast)."""
+        if self.half_t is None:
+            segs, tiles = [], 0
+            for q in self.params:
+                if q.dim() == 2:
+                    r, c = q.shape
+                    segs.append((self.offsets[id(q)], r, c, tiles))
+                    tiles += -(-r // 64) * -(-c // 64)
+            self._tsegs = torch.tensor(segs, dtype=torch.int64).to(self.device)
+            self._ttiles = tiles
+            self.bf16()
+            self.half_t = torch.empty(self.numel, dtype=torch.bfloat16, device=self.device)
+            self.refresh_half_t()
+        else:
+            self.bf16()
+        if p.dim() != 2:
+            raise ValueError("half_t_view: 2-D parameters only")
+        o = self.offsets[id(p)]
+        r, c = p.shape
+        return self.half_t[o:o + p.numel()].view(c, r)
 
     # ---- gradient side channel
     def grad_target(self, p) -> (torch.Tensor, bool):

@@ -199,6 +199,13 @@ int fer_adamw(float* param, const float* grad, float* exp_avg, float* exp_avg_sq
               const fer_adamw_segment* segs_device, int nsegs, int64_t max_seg_numel, float grad_scale,
               const float* clip_coef, const uint64_t* step_add, fer_stream_t stream);
 
+/* Transposed bf16 weight shadow (no reference counterpart: layout only). segs: device int64
+ * [nseg][4] = {offset, rows, cols, first_tile} into the flat buffers, first_tile the running
+ * count of 64x64 tiles (ceil(rows/64)*ceil(cols/64) per segment), total_tiles their sum:
+ * dst[off + c*rows + r] = src[off + r*cols + c]. The dgrad GEMMs read W^T K-contiguous. */
+int fer_transpose_bf16_segments(const void* src, void* dst, const int64_t* segs, int nseg, int64_t total_tiles,
+                                fer_stream_t stream);
+
 /* LatentAugment (`data/latent_dataset.py:6-49`) on a device batch x fp32 [B][LD], in place:
  * x += N(0, noise_std); x *= U(scale_lo, scale_hi) per sample; x *= (U(0,1) > mask_prob).
  * Counter-based draws keyed by seed (and the step counter below, when set). */

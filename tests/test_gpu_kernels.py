@@ -240,3 +240,24 @@ def test_cross_entropy_matches_torch():
             loss, dl = o.cross_entropy(logits.to(DEV), y.to(DEV), None if wt is None else wt.to(DEV), ls)
             assert abs(loss.item() - ref.item()) < 1e-5
             assert (dl.cpu() - lg.grad).abs().max().item() < 1e-6
+
+
+@pytest.mark.gpu
+def test_transposed_bf16_shadow():
+    """FlatParams.half_t_view == W^T of the bf16 shadow for ragged 2-D shapes, and it follows
+    in-place parameter updates (cast path) and the fused optimizer's refresh."""
+    from fervit.runtime import FlatParams
+
+    g = torch.Generator().manual_seed(5)
+    shapes = [(70, 130), (3072, 768), (1, 5), (7,), (65, 64), (2, 3, 4), (129, 1)]
+    ps = [torch.nn.Parameter(torch.randn(*s, generator=g).cuda()) for s in shapes]
+    flat = FlatParams(ps)
+    for p in ps:
+        if p.dim() == 2:
+            assert torch.equal(flat.half_t_view(p), flat.half_view(p).t().contiguous())
+    with torch.no_grad():
+        ps[1].mul_(-2.0)
+    t = flat.half_t_view(ps[1])
+    assert torch.equal(t, ps[1].data.to(torch.bfloat16).t().contiguous())
+    with pytest.raises(ValueError):
+        flat.half_t_view(ps[3])

@@ -35,6 +35,11 @@ def main():
     b1 = torch.zeros(F, device=dev)
     pre = torch.empty(M, F, device=dev, dtype=torch.bfloat16)
     gw = torch.empty(F, D, device=dev)
+    w2t, w1t = w2.t().contiguous(), w1.t().contiguous()  # [F, D], [D, F]
+    out_f = torch.empty(M, F, device=dev, dtype=torch.bfloat16)
+    out_d = torch.empty(M, D, device=dev, dtype=torch.bfloat16)
+    cs = torch.zeros(F, device=dev)
+    fused = dict(aux=pre, aux_act="gelu", dropout=0.1, seed=9, drop_ld=F, colsum=cs)
     cases = {
         "fc1 fwd plain": (lambda: ops.linear_fwd(x, w1), 2 * M * F * D, lambda: x @ w1.t()),
         "fc1 fwd +bias+gelu+drop+pre": (lambda: ops.linear_fwd(x, w1, b1, pre=pre, act="gelu", dropout=0.1, seed=7),
@@ -42,6 +47,11 @@ def main():
         "fc2 fwd plain (K=3072)": (lambda: ops.linear_fwd(h, w2), 2 * M * F * D, lambda: h @ w2.t()),
         "qkv fwd plain": (lambda: ops.linear_fwd(x, wqkv), 2 * M * 3 * D * D, lambda: x @ wqkv.t()),
         "fc2 dgrad (B MN)": (lambda: ops.linear_dgrad(x, w2), 2 * M * F * D, lambda: x @ w2),
+        "fc2 dgrad (B KC, W^T copy)": (lambda: ops.linear_fwd(x, w2t, out=out_f), 2 * M * F * D, None),
+        "fc2 dgrad fused (B MN)": (lambda: ops.linear_dgrad(x, w2, out=out_f, **fused), 2 * M * F * D, None),
+        "fc2 dgrad fused (B KC)": (lambda: ops.linear_fwd(x, w2t, out=out_f, **fused), 2 * M * F * D, None),
+        "fc1 dgrad +res (B MN, K=3072)": (lambda: ops.linear_dgrad(h, w1, out=out_d, res=x), 2 * M * F * D, None),
+        "fc1 dgrad +res (B KC, K=3072)": (lambda: ops.linear_fwd(h, w1t, out=out_d, res=x), 2 * M * F * D, None),
         "fc1 wgrad (MN,MN splitK)": (lambda: ops.linear_wgrad(dF, x, gw), 2 * M * F * D, lambda: dF.t() @ x),
     }
     only = os.environ.get("GB_ONLY")
