@@ -19,6 +19,7 @@ typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
 typedef __attribute__((ext_vector_type(4))) short short4_t;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
 typedef __attribute__((address_space(3))) void lds_void;
 
 enum { FER_ACT_NONE = 0, FER_ACT_GELU = 1, FER_ACT_RELU = 2 };
@@ -143,6 +144,13 @@ FER_DEV float wave_max(float v) {
 
 // ---------------------------------------------------------------- buffer rsrc
 // Raw buffer descriptor. Loads whose voffset >= num_records return 0: kernels
+// s_waitcnt vmcnt(N): all but this wave's N youngest vector-memory ops (loads, stores, LDS-DMA,
+// in issue order) are done.
+template <int N>
+FER_DEV void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
 // mask out-of-tile lanes by giving them FER_OOB as voffset.
 #define FER_OOB 0x80000000u
 FER_DEV __amdgpu_buffer_rsrc_t make_rsrc(const void* base) {

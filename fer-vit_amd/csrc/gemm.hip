@@ -244,11 +244,6 @@ FER_DEV bf16x8 read_frag(const char* lds_tile, int i0, int kk, int lane) {
   }
 }
 
-template <int N>
-FER_DEV void wait_vm() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
 template <int MT> struct Acc;
 template <> struct Acc<32> { typedef f32x16 T; };
 template <> struct Acc<16> { typedef f32x4 T; };

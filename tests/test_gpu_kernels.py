@@ -175,7 +175,8 @@ def attn_ref(qkv, B, N, H, dh, keep=None, p=0.0):
     return out, lse
 
 
-@pytest.mark.parametrize("N,H,dh", [(10, 8, 48), (19, 8, 64), (37, 12, 64), (197, 12, 64), (19, 6, 64)])
+@pytest.mark.parametrize("N,H,dh", [(10, 8, 48), (19, 8, 64), (37, 12, 64), (197, 12, 64), (19, 6, 64), (100, 4, 64),
+                                    (150, 3, 32), (250, 2, 64)])
 @pytest.mark.parametrize("dtype", ["bf16", "fp32"])
 @pytest.mark.parametrize("p", [0.0, 0.1])
 def test_attention_fwd_bwd(N, H, dh, dtype, p):
@@ -208,6 +209,11 @@ def test_attention_fwd_bwd(N, H, dh, dtype, p):
         a = dqkv.cpu().float()[:, j * D:(j + 1) * D]
         b = qr.grad[:, j * D:(j + 1) * D]
         assert rel_err(a, b) < 2 * tol, name
+    # deterministic: a second backward reproduces every bit (fixed-order dQ / bias sums)
+    dqkv2 = torch.empty_like(qd)
+    cs2 = torch.full((3 * D,), 0.5, device=DEV)
+    o.attention_bwd(qd, out, dd, lse, dqkv2, B, N, H, dh, dropout=p, seed=seed, colsum=cs2, colsum_accumulate=True)
+    assert torch.equal(dqkv2, dqkv) and torch.equal(cs2, cs)
 
 
 # ---------------------------------------------------------------------- misc

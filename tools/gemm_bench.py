@@ -44,6 +44,11 @@ def main():
         "fc1 fwd plain": (lambda: ops.linear_fwd(x, w1), 2 * M * F * D, lambda: x @ w1.t()),
         "fc1 fwd +bias+gelu+drop+pre": (lambda: ops.linear_fwd(x, w1, b1, pre=pre, act="gelu", dropout=0.1, seed=7),
                                          2 * M * F * D, None),
+        "fc1 fwd +bias": (lambda: ops.linear_fwd(x, w1, b1, out=out_f), 2 * M * F * D, None),
+        "fc1 fwd +bias+gelu": (lambda: ops.linear_fwd(x, w1, b1, out=out_f, act="gelu"), 2 * M * F * D, None),
+        "fc1 fwd +bias+relu+pre": (lambda: ops.linear_fwd(x, w1, b1, out=out_f, act="relu", pre=pre), 2 * M * F * D, None),
+        "fc1 fwd +bias+gelu+drop": (lambda: ops.linear_fwd(x, w1, b1, out=out_f, act="gelu", dropout=0.1, seed=7),
+                                    2 * M * F * D, None),
         "fc2 fwd plain (K=3072)": (lambda: ops.linear_fwd(h, w2), 2 * M * F * D, lambda: h @ w2.t()),
         "qkv fwd plain": (lambda: ops.linear_fwd(x, wqkv), 2 * M * 3 * D * D, lambda: x @ wqkv.t()),
         "fc2 dgrad (B MN)": (lambda: ops.linear_dgrad(x, w2), 2 * M * F * D, lambda: x @ w2),
