@@ -261,6 +261,8 @@ FER_DEV typename Acc<MT>::T mfma(bf16x8 a, bf16x8 b, typename Acc<MT>::T c) {
 template <int BM, int BN, int WM, int WN, int MT, int EPC, int SMEMB, typename AccT, int FN, int FM>
 FER_DEV void tile_epilogue(const GemmArgs& g, const EpiArgs& e, AccT (&acc)[FN][FM], char* smem, int m0, int n0,
                            int ks, int wm, int wn, int lane) {
+  int tid_ = threadIdx.x;  // laundered: not hoisted out of a persistent tile loop
+  asm volatile("" : "+v"(tid_));
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int NQ = MT == 32 ? 4 : 1;
   const int lr = MT == 32 ? (lane & 31) : (lane & 15);
@@ -305,8 +307,8 @@ FER_DEV void tile_epilogue(const GemmArgs& g, const EpiArgs& e, AccT (&acc)[FN][
   // LDS by LDS-DMA while chunk h is processed. vmcnt retires loads, stores and DMA in issue
   // order, so each DMA is issued BEFORE the previous chunk's stores... and waited for with a
   // count that skips exactly those stores; the item loop itself never waits on memory.
-  const int tc = (threadIdx.x % C8) * 8, tr = threadIdx.x / C8;
-  const int wave = threadIdx.x >> 6;
+  const int tc = (tid_ % C8) * 8, tr = tid_ / C8;
+  const int wave = tid_ >> 6;
   const long n = n0 + tc;
   const bool nok = n < g.N;  // N % 8 == 0 on this path (checked by the host)
   f32x4 b0 = f32x4{0.f, 0.f, 0.f, 0.f}, b1 = b0;
@@ -399,7 +401,7 @@ FER_DEV void tile_epilogue(const GemmArgs& g, const EpiArgs& e, AccT (&acc)[FN][
     *(f32x4*)(red + tr * BN + tc) = cs0;
     *(f32x4*)(red + tr * BN + tc + 4) = cs1;
     __syncthreads();
-    for (int c = threadIdx.x; c < BN; c += NT) {
+    for (int c = tid_; c < BN; c += NT) {
       float t = 0.f;
       for (int r = 0; r < RPI; ++r) t += red[r * BN + c];
       if (n0 + c < g.N) g.cs_part[(long)(m0 / BM) * g.N + n0 + c] = t;
@@ -699,20 +701,22 @@ struct UnitPlan {
 };
 
 template <bool AKC, bool BKC, int MT>
-__global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmArgs g, EpiArgs e) {
+FER_DEV void tile_8ph(const GemmArgs& g, const EpiArgs& e, int bid, char* smem) {
   typedef typename Acc<MT>::T AccT;
   constexpr int UNIT = 16384, BUF = 4 * UNIT;  // A0 A1 B0 B1
   constexpr int FM = 128 / MT, FN = 64 / MT;   // MFMA blocks per wave (rows, cols)
   constexpr int QJ = FM / 2, QI = FN / 2;      // per quadrant
   constexpr int KS = 64 / (MT == 32 ? 16 : 32);  // MFMA K-steps per K-tile
-  __shared__ __attribute__((aligned(1024))) char smem[2 * BUF];
-
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // launder the thread index: lane-derived addressing is recomputed per tile instead of being
+  // hoisted out of the persistent loop (hoisting pushed the kernel past 256 VGPRs)
+  int tid = threadIdx.x;
+  asm volatile("" : "+v"(tid));
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
 
   int tm, tn;
-  tile_of(blockIdx.x, g.tiles_m, g.tiles_n, tm, tn);
+  tile_of(bid, g.tiles_m, g.tiles_n, tm, tn);
   const int m0 = tm * 256, n0 = tn * 256;
   const int ks = blockIdx.y;
   const int kbeg = ks * g.k_chunk;
@@ -811,6 +815,21 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmArgs g, EpiArgs e)
   tile_epilogue<256, 256, 2, 4, MT, 2, 2 * BUF>(g, e, acc, smem, m0, n0, ks, wr, wc, lane);
 }
 
+// Persistent launch (one workgroup per CU, tiles bid, bid + grid, ...: the XCD-aware tile order
+// is kept since grid % 8 == 0). A workgroup goes from one tile's epilogue stores straight into
+// the next tile's operand DMA, so the store drain overlaps the next tile's first loads instead
+// of sitting between a workgroup's exit and its successor's launch.
+template <bool AKC, bool BKC, int MT>
+__global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmArgs g, EpiArgs e) {
+  __shared__ __attribute__((aligned(1024))) char smem[8 * 16384];
+  const int ntiles = g.tiles_m * g.tiles_n;
+#pragma unroll 1
+  for (int bid = blockIdx.x; bid < ntiles; bid += gridDim.x) {
+    tile_8ph<AKC, BKC, MT>(g, e, bid, smem);
+    __syncthreads();  // every wave is done with the epilogue's LDS before the next tile's DMA
+  }
+}
+
 // Ordered (deterministic) split-K reduction + epilogue.
 template <typename T>
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ ws, int splits, long M, long N,
@@ -892,7 +911,17 @@ template <bool AKC, bool BKC, int MT>
 static int launch_8ph(GemmArgs g, const EpiArgs& e, hipStream_t st) {
   g.tiles_m = (g.M + 255) / 256;
   g.tiles_n = (g.N + 255) / 256;
-  dim3 grid(g.tiles_m * g.tiles_n, g.splits);
+  static const int ncu = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      n = 256;
+    return n > 0 ? n : 256;
+  }();
+  static const bool persist = getenv("FERVIT_GEMM_NOPERSIST") == nullptr;  // A/B switch
+  const int ntiles = g.tiles_m * g.tiles_n;
+  const int gx = persist ? std::min(ntiles, std::max(8, ncu / 8 * 8)) : ntiles;
+  dim3 grid(gx, g.splits);
   hipLaunchKernelGGL((gemm_8ph_kernel<AKC, BKC, MT>), grid, dim3(512), 0, st, g, e);
   return 0;
 }
