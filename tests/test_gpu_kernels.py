@@ -81,6 +81,13 @@ def test_gemm_persistent_many_tiles(M, N, K):
     assert rel_err(y3, ref + b + res.float()) < 1e-2
     # deterministic across calls
     assert torch.equal(o.linear_fwd(x, w), y)
+    # dropout keep bits (hashed inside the main loop): exact pattern against the host replica,
+    # on a strictly positive pre-activation so that an output is 0 iff it was dropped
+    xp, wp = x.abs() + 0.01, (w.abs() + 0.01).to(torch.bfloat16)
+    xp = xp.to(torch.bfloat16)
+    yd = o.linear_fwd(xp, wp, act="relu", dropout=0.1, seed=77)
+    keep = keep_mask(77, (M, N), 0.1).to(DEV)
+    assert torch.equal(yd != 0, keep)
 
 
 @pytest.mark.parametrize("cfg", list(range(10)))
