@@ -57,7 +57,9 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, lo
 }
 
 // partial layout: ws[blk][3][D]
-template <typename T>
+// VPL = vectors of 4 per lane = ceil(D / 256): sized per D so that D = 768 keeps the register
+// sets (two rows in flight + the column partials) at 3 waves per SIMD instead of 2.
+template <typename T, int VPL>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, long lddy, const T* __restrict__ x,
                                                      long ldx, const float* __restrict__ mean,
                                                      const float* __restrict__ rstd, const float* __restrict__ g,
@@ -66,20 +68,20 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, l
                                                      uint32_t thr, float dscale, uint64_t seed,
                                                      float* __restrict__ part, int want_part, int M, int D) {
   seed = step_seed(seed);
-  __shared__ float red[4][LN_VPL * 256];  // one partial at a time: 16 KB keeps 4+ blocks/CU
+  __shared__ float red[4][VPL * 256];  // one partial at a time
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int nv = D >> 2;
-  f32x4 pg[LN_VPL], pb[LN_VPL], pd[LN_VPL];
+  f32x4 pg[VPL], pb[VPL], pd[VPL];
 #pragma unroll
-  for (int i = 0; i < LN_VPL; ++i) pg[i] = pb[i] = pd[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int i = 0; i < VPL; ++i) pg[i] = pb[i] = pd[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   // Rows are processed in pairs with two register sets: the loads of the next row are issued
   // before the stores of the current one. (vmcnt retires loads and stores in issue order: a
   // load issued after a store would make every use wait for that store to drain.)
   typedef typename Raw4<T>::type R4;
-  R4 dyA[LN_VPL], xA[LN_VPL], rA[LN_VPL], dyB[LN_VPL], xB[LN_VPL], rB[LN_VPL];
-  auto load_row = [&](long row, R4(&dyr)[LN_VPL], R4(&xr)[LN_VPL], R4(&rr)[LN_VPL]) {
+  R4 dyA[VPL], xA[VPL], rA[VPL], dyB[VPL], xB[VPL], rB[VPL];
+  auto load_row = [&](long row, R4(&dyr)[VPL], R4(&xr)[VPL], R4(&rr)[VPL]) {
 #pragma unroll
-    for (int i = 0; i < LN_VPL; ++i) {
+    for (int i = 0; i < VPL; ++i) {
       const int c = lane + i * 64;
       if (c < nv) {
         dyr[i] = *(const R4*)(dy + row * lddy + c * 4);
@@ -88,13 +90,13 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, l
       }
     }
   };
-  auto proc_row = [&](long row, const R4(&dyr)[LN_VPL], const R4(&xr)[LN_VPL], const R4(&rr)[LN_VPL]) {
+  auto proc_row = [&](long row, const R4(&dyr)[VPL], const R4(&xr)[VPL], const R4(&rr)[VPL]) {
     const float mu = mean[row], rs = rstd[row];
     const long gr = grows > 1 ? ((row / rdiv) % grows) * D : 0;
-    f32x4 xh[LN_VPL], gy[LN_VPL], dyv[LN_VPL];
+    f32x4 xh[VPL], gy[VPL], dyv[VPL];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-    for (int i = 0; i < LN_VPL; ++i) {
+    for (int i = 0; i < VPL; ++i) {
       const int c = lane + i * 64;
       if (c < nv) {
         dyv[i] = raw4_to_f(dyr[i]);
@@ -110,7 +112,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, l
     s1 = wave_sum(s1) / D;
     s2 = wave_sum(s2) / D;
 #pragma unroll
-    for (int i = 0; i < LN_VPL; ++i) {
+    for (int i = 0; i < VPL; ++i) {
       const int c = lane + i * 64;
       if (c < nv) {
         f32x4 d = (gy[i] - s1 - xh[i] * s2) * rs;
@@ -142,7 +144,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, l
   for (int k = 0; k < 3; ++k) {
     if (k) __syncthreads();
 #pragma unroll
-    for (int i = 0; i < LN_VPL; ++i) *(f32x4*)&red[w][(lane + i * 64) * 4] = k == 0 ? pg[i] : (k == 1 ? pb[i] : pd[i]);
+    for (int i = 0; i < VPL; ++i) *(f32x4*)&red[w][(lane + i * 64) * 4] = k == 0 ? pg[i] : (k == 1 ? pb[i] : pd[i]);
     __syncthreads();
     for (int c = threadIdx.x; c < D; c += 256)
       part[((long)blockIdx.x * 3 + k) * D + c] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
@@ -206,15 +208,24 @@ extern "C" int fer_layernorm_bwd(int dtype, const void* dy, int64_t lddy, const 
   const int nblk = ln_bwd_blocks(M);
   if (want && (!ws || ws_bytes < fer_layernorm_bwd_ws(M, D))) return set_error("layernorm_bwd: workspace too small");
   hipStream_t st = (hipStream_t)stream;
-  if (dtype == FER_BF16)
-    hipLaunchKernelGGL(ln_bwd_kernel<bf16>, dim3(nblk), dim3(256), 0, st, (const bf16*)dy, (long)lddy,
-                       (const bf16*)x, (long)ldx, mean, rstd, gamma, gamma_rows, row_div, (const bf16*)res, (long)ldr,
-                       (bf16*)dx, (long)lddx, (bf16*)dx_drop, drop_thresh, drop_scale, seed, ws, (int)want, M, D);
-  else
-    hipLaunchKernelGGL(ln_bwd_kernel<float>, dim3(nblk), dim3(256), 0, st, (const float*)dy, (long)lddy,
-                       (const float*)x, (long)ldx, mean, rstd, gamma, gamma_rows, row_div, (const float*)res,
-                       (long)ldr, (float*)dx, (long)lddx, (float*)dx_drop, drop_thresh, drop_scale, seed, ws,
-                       (int)want, M, D);
+#define FER_LN_BWD(VP)                                                                                       \
+  if (dtype == FER_BF16)                                                                                     \
+    hipLaunchKernelGGL((ln_bwd_kernel<bf16, VP>), dim3(nblk), dim3(256), 0, st, (const bf16*)dy, (long)lddy,  \
+                       (const bf16*)x, (long)ldx, mean, rstd, gamma, gamma_rows, row_div, (const bf16*)res,   \
+                       (long)ldr, (bf16*)dx, (long)lddx, (bf16*)dx_drop, drop_thresh, drop_scale, seed, ws,   \
+                       (int)want, M, D);                                                                     \
+  else                                                                                                       \
+    hipLaunchKernelGGL((ln_bwd_kernel<float, VP>), dim3(nblk), dim3(256), 0, st, (const float*)dy,           \
+                       (long)lddy, (const float*)x, (long)ldx, mean, rstd, gamma, gamma_rows, row_div,       \
+                       (const float*)res, (long)ldr, (float*)dx, (long)lddx, (float*)dx_drop, drop_thresh,   \
+                       drop_scale, seed, ws, (int)want, M, D);
+  switch ((D + 255) / 256) {
+    case 1: FER_LN_BWD(1) break;
+    case 2: FER_LN_BWD(2) break;
+    case 3: FER_LN_BWD(3) break;
+    default: FER_LN_BWD(4) break;
+  }
+#undef FER_LN_BWD
   int rc = hip_check("layernorm_bwd");
   if (rc || !want) return rc;
   part_reduce(ws, nblk, 3L * D, 3 * D, D, dgamma, dbeta, dbias, accumulate, nullptr, st);

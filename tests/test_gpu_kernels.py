@@ -159,7 +159,7 @@ def test_gemm_keep_rate():
 
 # ---------------------------------------------------------------------- LayerNorm
 @pytest.mark.parametrize("dtype", ["bf16", "fp32"])
-@pytest.mark.parametrize("D", [384, 512, 768])
+@pytest.mark.parametrize("D", [128, 384, 512, 768, 1024])
 def test_layernorm_fwd_bwd(dtype, D):
     o = ops()
     M = 1000
