@@ -996,9 +996,10 @@ int gemm_launch(const GemmDesc& d, const EpiArgs& e_in, hipStream_t st) {
   const long b_bytes = (d.b_kc ? (long)(d.N - 1) * d.ldb + d.K : (long)(d.K - 1) * d.ldb + d.N) * 2;
   if (a_bytes >= 0x7FFFFFF0L || b_bytes >= 0x7FFFFFF0L) return set_error("gemm: operand exceeds 2 GiB");
 
-  // Configuration (measured on MI355X, tools/gemm_bench.py): the 8-phase 256^2 kernel whenever
-  // the grid (with split-K) gives it >= 128 workgroups (the BK=32 ring for the MN x MN weight
-  // gradient: 261 vs 283 us on fc1), else 128^2 tiles at 2 blocks per CU.
+  // Configuration (measured on MI355X, tools/gemm_bench.py, tools/gemm_small_bench.py): the
+  // 8-phase 256^2 kernel for grids of >= 256 such tiles or K >= 8192 (the BK=32 ring for the
+  // MN x MN weight gradient: 261 vs 283 us on fc1); grids smaller than the CU count (the latent
+  // w+ and 48 px configs) run 128^2 tiles at two blocks per CU (latent fc2 fwd 37 vs 45 us).
   // Split-K (weight gradients, K = tokens) targets one 256^2 workgroup per CU.
   const long t256 = (long)((d.M + 255) / 256) * ((d.N + 255) / 256);
   const long t128 = (long)((d.M + 127) / 128) * ((d.N + 127) / 128);
@@ -1009,7 +1010,12 @@ int gemm_launch(const GemmDesc& d, const EpiArgs& e_in, hipStream_t st) {
     return (int)std::max<long>(1, std::min<long>({target / tiles, d.K / 256, (long)max_splits}));
   };
   int cfg = forced_cfg();
-  if (cfg < 0) cfg = t256 * splits_for(t256, 256) >= 128 ? (!d.a_kc && !d.b_kc ? 5 : 8) : 3;
+  if (cfg < 0) {
+    if (d.K >= 8192 || t256 >= 256)  // big grids, and token-long weight gradients (split-K fills the GPU)
+      cfg = t256 * splits_for(t256, 256) >= 128 ? (!d.a_kc && !d.b_kc ? 5 : 8) : 3;
+    else  // fewer 256^2 tiles than CUs (latent / 48 px configs): 128^2 tiles, two workgroups per CU
+      cfg = 3;
+  }
   int splits = cfg_is_256(cfg) ? splits_for(t256, 256) : splits_for(t128, 512);
   g.splits = splits;
   g.k_chunk = splits > 1 ? (((d.K + splits - 1) / splits + BK - 1) / BK) * BK : d.K;

@@ -1,0 +1,34 @@
+"""GEMM configurations on the latent-config shapes (LatentViT bs=256: M = 256*19 = 4864 rows,
+E=512, F=2048): forward, dgrad (transposed weights), wgrad; run once per FERVIT_GEMM_CFG."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "fer-vit_amd"))
+import torch  # noqa: E402
+
+from fervit import ops  # noqa: E402
+from gemm_bench import timeit  # noqa: E402
+
+
+def main():
+    M, E, F = 256 * 19, 512, 2048
+    g = torch.Generator(device="cuda").manual_seed(0)
+    r = lambda *s: torch.randn(*s, device="cuda", generator=g).to(torch.bfloat16)
+    x, h = r(M, E), r(M, F)
+    shapes = {"qkv fwd": (x, r(3 * E, E)), "out fwd": (x, r(E, E)), "fc1 fwd": (x, r(F, E)), "fc2 fwd": (h, r(E, F))}
+    b = {k: torch.zeros(w.shape[0], device="cuda") for k, (a, w) in shapes.items()}
+    tag = os.environ.get("FERVIT_GEMM_CFG", "auto")
+    tot = 0.0
+    for k, (a, w) in shapes.items():
+        t = min(timeit(lambda: ops.linear_fwd(a, w, b[k], act="relu")) for _ in range(3))
+        tot += t
+        fl = 2 * a.shape[0] * a.shape[1] * w.shape[0]
+        print(f"[cfg {tag}] {k:8s} {t * 1e3:7.1f} us {fl / t / 1e9:6.1f} TF", flush=True)
+    gw = torch.empty(F, E, device="cuda")
+    t = min(timeit(lambda: ops.linear_wgrad(h, x, gw)) for _ in range(3))
+    print(f"[cfg {tag}] fc1 wgrad {t * 1e3:7.1f} us  (sum fwd {tot * 1e3:.1f} us)", flush=True)
+
+
+if __name__ == "__main__":
+    main()

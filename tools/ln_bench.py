@@ -13,7 +13,7 @@ from gemm_bench import timeit  # noqa: E402
 
 
 def main():
-    M, D = 256 * 197, 768
+    M, D = int(os.environ.get("LN_M", 256 * 197)), int(os.environ.get("LN_D", 768))
     g = torch.Generator(device="cuda").manual_seed(0)
     x = torch.randn(M, D, device="cuda", generator=g).to(torch.bfloat16)
     dy = torch.randn(M, D, device="cuda", generator=g).to(torch.bfloat16)
