@@ -45,6 +45,12 @@ CONFIGS = {
     "image_vit_48": ("image", dict(img_size=48, patch_size=16, embed_dim=384, depth=6, heads=8, mlp_dim=1536,
                                    dropout=0.1), 64, (3, 48, 48),
                      "image_vit d6/h8 e384, 48x48 FER-2013-shaped synthetic, bs=64, train step"),
+    "hybrid_latent_vit": ("hybrid", dict(), 256, (18, 512),
+                          "hybrid_latent_vit timm-B/16 blocks frozen + adapter 64, w+ latents, bs=256/GPU, "
+                          "train step (CE, AdamW on the trainable parameters)"),
+    "expression_aware_vit": ("expr", dict(), 256, (18, 512),
+                             "expression_aware_vit: decomposer (7 seeded unit directions, all_classes, "
+                             "expr_only) + SPE + LEAM + hybrid timm-B/16 frozen + adapter 64, bs=256/GPU"),
 }
 
 
@@ -59,18 +65,36 @@ def build(cfg_name, device):
     from fervit.optim import FusedAdamW
 
     kind, ctor, B, shape, desc = CONFIGS[cfg_name]
+    ls = 0.1
     if kind == "image":
         from models_fer_vit.image_vit import ImageViT
 
         m = ImageViT(num_classes=7, **ctor)
-    else:
+    elif kind == "latent":
         from models_fer_vit.latent_vit import LatentViT
 
         m = LatentViT(**ctor)
+    else:  # SURVEY §8(d) cfg4 / cfg5 (the hybrid trainers use no label smoothing)
+        from models_fer_vit.hybrid_latent_vit import create_hybrid_latent_vit
+
+        ls = 0.0
+        vit = create_hybrid_latent_vit(model_size="base", use_pretrained=False, freeze_transformer=True,
+                                       use_adapter=True, adapter_dim=64)
+        if kind == "hybrid":
+            m = vit
+        else:
+            from models_fer_vit.expression_aware_vit import ExpressionAwareViT
+            from models_fer_vit.latent_decomposer import LatentDecomposer
+
+            g = torch.Generator().manual_seed(7)
+            dirs = {c: torch.nn.functional.normalize(torch.randn(18, 512, generator=g).view(-1), dim=0).view(18, 512)
+                    for c in range(7)}
+            m = ExpressionAwareViT(LatentDecomposer(dirs), vit, output_mode="expr_only",
+                                   decompose_mode="all_classes", use_spe=True, use_leam=True)
     m = m.to(device)
     m.set_precision("bf16")
-    opt = FusedAdamW(m.parameters(), lr=1e-3, weight_decay=0.05, model=m)
-    return m, opt, CrossEntropyLoss(label_smoothing=0.1), B, shape, desc
+    opt = FusedAdamW([p for p in m.parameters() if p.requires_grad], lr=1e-3, weight_decay=0.05, model=m)
+    return m, opt, CrossEntropyLoss(label_smoothing=ls), B, shape, desc
 
 
 class GemmProbe:
@@ -253,9 +277,15 @@ def main():
         D, L, F = ctor["embed_dim"], ctor["depth"], ctor["mlp_dim"]
         N = (ctor["img_size"] // ctor["patch_size"]) ** 2 + 1
         flops_img = gemm_flops_per_img(D, L, F, N, 3 * ctor["patch_size"] ** 2, N - 1)
-    else:
+    elif kind == "latent":
         D, L, F, N = 512, 6, 2048, 19
         flops_img = gemm_flops_per_img(D, L, F, N) + 3 * 2 * 18 * 512 * 512
+    else:
+        # frozen trunk: fwd + dgrad only (2x its fwd); trainable input_proj, adapters, head: 3x
+        D, L, F, N = 768, 12, 3072, 19
+        trunk = gemm_flops_per_img(D, L, F, N) // 3
+        adapters = L * 2 * N * (2 * D * 64)
+        flops_img = 2 * trunk + 3 * (adapters + 2 * 18 * 512 * D + 2 * D * 7)
     probe = GemmProbe(B * N, F, D)
     ops.LAUNCH_PROBE = probe
 
