@@ -48,8 +48,8 @@ FER_DEV void epi8_bf16(const EpiArgs& e, long m, long n, f32x4& v0, f32x4& v1, f
   if (e.act == FER_ACT_GELU) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      v0[r] = gelu_erf(v0[r]);
-      v1[r] = gelu_erf(v1[r]);
+      v0[r] = gelu_erf_fast(v0[r]);
+      v1[r] = gelu_erf_fast(v1[r]);
     }
   } else if (e.act == FER_ACT_RELU) {
 #pragma unroll
