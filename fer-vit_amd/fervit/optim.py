@@ -118,10 +118,16 @@ class FusedAdamW(torch.optim.Optimizer):
 
     @staticmethod
     def _upload(segs, flat):
+        """Segment table -> device through pinned memory, stream-ordered: a pageable blocking
+        copy would make the host wait for the whole step's kernels every optimizer step, and
+        the GPU then idle while the next step's first launches are issued."""
         arr = (AdamWSegment * len(segs))(*[AdamWSegment(*s) for s in segs])
         host = torch.frombuffer(bytearray(ctypes.string_at(ctypes.addressof(arr), ctypes.sizeof(arr))),
                                 dtype=torch.uint8)
-        return host.to(flat.data.device, non_blocking=False)
+        if flat.data.is_cuda:
+            host = host.pin_memory()  # the caching host allocator keeps it until the copy is done
+            return host.to(flat.data.device, non_blocking=True)
+        return host.to(flat.data.device)
 
     @torch.no_grad()
     def step(self, closure=None):

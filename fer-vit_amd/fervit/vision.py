@@ -77,7 +77,11 @@ class GPUImageTransform:
             hv[o:o + a.nbytes] = a.reshape(-1)
         hwc = np.array([s for a in arrs for s in a.shape], dtype=np.int32)
         dev = device or torch.device("cuda", torch.cuda.current_device())
-        return (host.to(dev, non_blocking=True), torch.from_numpy(offs).to(dev), torch.from_numpy(hwc).to(dev))
+        pin = torch.cuda.is_available()
+        offs_t, hwc_t = torch.from_numpy(offs), torch.from_numpy(hwc)
+        if pin:
+            offs_t, hwc_t = offs_t.pin_memory(), hwc_t.pin_memory()
+        return (host.to(dev, non_blocking=True), offs_t.to(dev, non_blocking=True), hwc_t.to(dev, non_blocking=True))
 
     def __call__(self, images: Sequence, params: Optional[torch.Tensor] = None) -> torch.Tensor:
         B, S = len(images), self.img_size
