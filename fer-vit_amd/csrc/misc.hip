@@ -632,6 +632,7 @@ __global__ __launch_bounds__(256) void transpose_segs_kernel(const uint16_t* __r
                                                              uint16_t* __restrict__ dst,
                                                              const int64_t* __restrict__ segs, int nseg) {
   __shared__ uint32_t tile[64][33];  // 64 rows x 64 bf16 (as 32 pairs), +1 word pad
+  __shared__ __attribute__((aligned(16))) uint16_t t16x[64 * 72];  // fast path: rows padded by 16 B
   const long t = blockIdx.x;
   int lo = 0, hi = nseg - 1;
   while (lo < hi) {
@@ -645,6 +646,30 @@ __global__ __launch_bounds__(256) void transpose_segs_kernel(const uint16_t* __r
   const uint16_t* s = src + off;
   uint16_t* d = dst + off;
   const int tid = threadIdx.x;
+  if (r0 + 64 <= rows && c0 + 64 <= cols && rows % 8 == 0 && cols % 8 == 0 && off % 8 == 0) {
+    // full, 16-byte aligned tile: 16-byte loads along input rows, 16-byte stores along output rows
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int i = tid + k * 256, r = i >> 3, ch = i & 7;
+      const uint4 v = *(const uint4*)(s + (r0 + r) * cols + c0 + ch * 8);
+      *(uint4*)(t16x + r * 72 + ch * 8) = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int i = tid + k * 256, c = i >> 3, rc = i & 7;  // output row c, 8 input rows from rc*8
+      uint16_t e[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) e[j] = t16x[(rc * 8 + j) * 72 + c];
+      uint4 o;
+      o.x = e[0] | ((uint32_t)e[1] << 16);
+      o.y = e[2] | ((uint32_t)e[3] << 16);
+      o.z = e[4] | ((uint32_t)e[5] << 16);
+      o.w = e[6] | ((uint32_t)e[7] << 16);
+      *(uint4*)(d + (c0 + c) * rows + r0 + rc * 8) = o;
+    }
+    return;
+  }
   // load: row r, column pair cp (2 bf16); 64 x 32 pairs = 2048 / 256 threads
   for (int i = tid; i < 64 * 32; i += 256) {
     const int r = i >> 5, cp = i & 31;

@@ -25,9 +25,13 @@ def main():
         tot += t
         fl = 2 * a.shape[0] * a.shape[1] * w.shape[0]
         print(f"[cfg {tag}] {k:8s} {t * 1e3:7.1f} us {fl / t / 1e9:6.1f} TF", flush=True)
-    gw = torch.empty(F, E, device="cuda")
-    t = min(timeit(lambda: ops.linear_wgrad(h, x, gw)) for _ in range(3))
-    print(f"[cfg {tag}] fc1 wgrad {t * 1e3:7.1f} us  (sum fwd {tot * 1e3:.1f} us)", flush=True)
+    print(f"[cfg {tag}] sum fwd {tot * 1e3:.1f} us", flush=True)
+    dys = {"fc1": (h, x), "fc2": (x, h), "qkv": (r(M, 3 * E), x), "out": (x, x)}
+    for k, (dy, a) in dys.items():
+        gw = torch.empty(dy.shape[1], a.shape[1], device="cuda")
+        for split in (True, False):
+            t = min(timeit(lambda: ops.linear_wgrad(dy, a, gw, split_ws=split)) for _ in range(3))
+            print(f"[cfg {tag}] {k} wgrad split={int(split)} {t * 1e3:7.1f} us", flush=True)
 
 
 if __name__ == "__main__":
