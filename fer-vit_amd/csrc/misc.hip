@@ -91,7 +91,43 @@ __global__ __launch_bounds__(256) void im2col_kernel(const float* __restrict__ x
   }
 }
 
+// 4 consecutive kw per thread (P % 4 == 0, Ww % 4 == 0, ldc % 4 == 0): one 16-byte input load
+// and one 4-element store, 32-bit index arithmetic (total / 4 < 2^31, checked by the host).
+template <typename T>
+__global__ __launch_bounds__(256) void im2col4_kernel(const float* __restrict__ x, int B, int C, int Hh, int Ww,
+                                                      int P, T* __restrict__ cols, long ldc) {
+  const int gh = Hh / P, gw = Ww / P, K = C * P * P, K4 = K >> 2, PP = P * P;
+  const int total = B * gh * gw * K4;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+    const int k = (i % K4) * 4;
+    const int tok = i / K4;
+    const int gx = tok % gw, gy = (tok / gw) % gh, b = tok / (gw * gh);
+    const int c = k / PP, kh = (k / P) % P, kw = k % P;
+    const f32x4 v = *(const f32x4*)(x + (((long)b * C + c) * Hh + gy * P + kh) * Ww + gx * P + kw);
+    store4<T>(cols + (long)tok * ldc + k, v);
+  }
+}
+
 // ------------------------------------------------------------------ tokens
+// 4 consecutive d per thread (D % 4 == 0); dropout keep bits identical to the scalar form.
+template <typename T>
+__global__ __launch_bounds__(256) void tokens_fwd4_kernel(const T* __restrict__ emb, const float* __restrict__ cls,
+                                                          const float* __restrict__ pos, T* __restrict__ t, int B,
+                                                          int n, int D, uint32_t thr, float dscale, uint64_t seed) {
+  seed = step_seed(seed);
+  const int N = n + 1, D4 = D >> 2;
+  const long total = (long)B * N * D4;
+  for (long i4 = blockIdx.x * 256L + threadIdx.x; i4 < total; i4 += (long)gridDim.x * 256L) {
+    const int d = (int)(i4 % D4) * 4;
+    const long row = i4 / D4;
+    const int tk = (int)(row % N), b = (int)(row / N);
+    f32x4 v = tk == 0 ? *(const f32x4*)(cls + d) : load4<T>(emb + ((long)b * n + tk - 1) * D + d);
+    v += *(const f32x4*)(pos + (long)tk * D + d);
+    if (thr) drop4(seed, (uint32_t)(row * D + d), thr, dscale, v);
+    store4<T>(t + row * D + d, v);
+  }
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void tokens_fwd_kernel(const T* __restrict__ emb, const float* __restrict__ cls,
                                                          const float* __restrict__ pos, T* __restrict__ t, int B,
@@ -252,6 +288,15 @@ __global__ void head_bwd_final(const float* __restrict__ part, int B, int C, int
   else { o = dlb; k = j - (long)C * D - C - D; }
   if (!o) return;
   o[k] = accumulate ? o[k] + s : s;
+}
+template <typename T>
+__global__ void zero_rows4_kernel(T* __restrict__ dt, long rows, int D_ld, int D, long stride_keep) {
+  const int D4 = D >> 2;
+  const long total = rows * (long)D4;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256L) {
+    const long r = i / D4;
+    if (r % stride_keep) store4<T>(dt + r * D_ld + (i % D4) * 4, f32x4{0.f, 0.f, 0.f, 0.f});
+  }
 }
 template <typename T>
 __global__ void zero_rows_kernel(T* __restrict__ dt, long rows, int D_ld, int D, long stride_keep) {
@@ -730,6 +775,15 @@ extern "C" int fer_im2col_patch(int dtype, const float* x, int B, int C, int Hh,
   const long total = (long)B * (Hh / P) * (Ww / P) * C * P * P;
   if (total <= 0) return 0;
   hipStream_t st = (hipStream_t)stream;
+  if (P % 4 == 0 && Ww % 4 == 0 && ldc % 4 == 0 && total / 4 < 0x7FFFFFFFL && (uintptr_t)x % 16 == 0) {
+    if (dtype == FER_BF16)
+      hipLaunchKernelGGL(im2col4_kernel<bf16>, dim3(grid_for(total / 4)), dim3(256), 0, st, x, B, C, Hh, Ww, P,
+                         (bf16*)cols, (long)ldc);
+    else
+      hipLaunchKernelGGL(im2col4_kernel<float>, dim3(grid_for(total / 4)), dim3(256), 0, st, x, B, C, Hh, Ww, P,
+                         (float*)cols, (long)ldc);
+    return hip_check("im2col_patch");
+  }
   if (dtype == FER_BF16)
     hipLaunchKernelGGL(im2col_kernel<bf16>, dim3(grid_for(total)), dim3(256), 0, st, x, B, C, Hh, Ww, P, (bf16*)cols,
                        (long)ldc);
@@ -745,6 +799,15 @@ extern "C" int fer_tokens_fwd(int dtype, const void* emb, const float* cls, cons
   if (total <= 0) return 0;
   if (check_drop_range(drop_thresh, total, "tokens_fwd: dropout over >= 2^32 elements")) return -1;
   hipStream_t st = (hipStream_t)stream;
+  if (D % 4 == 0) {
+    if (dtype == FER_BF16)
+      hipLaunchKernelGGL(tokens_fwd4_kernel<bf16>, dim3(grid_for(total / 4)), dim3(256), 0, st, (const bf16*)emb, cls,
+                         pos, (bf16*)t, B, n, D, drop_thresh, drop_scale, seed);
+    else
+      hipLaunchKernelGGL(tokens_fwd4_kernel<float>, dim3(grid_for(total / 4)), dim3(256), 0, st, (const float*)emb,
+                         cls, pos, (float*)t, B, n, D, drop_thresh, drop_scale, seed);
+    return hip_check("tokens_fwd");
+  }
   if (dtype == FER_BF16)
     hipLaunchKernelGGL(tokens_fwd_kernel<bf16>, dim3(grid_for(total)), dim3(256), 0, st, (const bf16*)emb, cls, pos,
                        (bf16*)t, B, n, D, drop_thresh, drop_scale, seed);
@@ -805,7 +868,15 @@ extern "C" int fer_head_bwd(int dtype, const void* t, int64_t row_stride, const 
   if (D > 1024) return set_error("head_bwd: D <= 1024");
   if (!ws || ws_bytes < fer_head_bwd_ws(B, D, C)) return set_error("head_bwd: workspace too small");
   hipStream_t st = (hipStream_t)stream;
-  if (zero_rest) {
+  if (zero_rest && D % 4 == 0 && D_ld % 4 == 0) {
+    const long total = (long)rows_total * D / 4;
+    if (dtype == FER_BF16)
+      hipLaunchKernelGGL(zero_rows4_kernel<bf16>, dim3(grid_for(total)), dim3(256), 0, st, (bf16*)dt, (long)rows_total,
+                         D_ld, D, (long)(row_stride / D_ld));
+    else
+      hipLaunchKernelGGL(zero_rows4_kernel<float>, dim3(grid_for(total)), dim3(256), 0, st, (float*)dt,
+                         (long)rows_total, D_ld, D, (long)(row_stride / D_ld));
+  } else if (zero_rest) {
     const long total = (long)rows_total * D;
     if (dtype == FER_BF16)
       hipLaunchKernelGGL(zero_rows_kernel<bf16>, dim3(grid_for(total)), dim3(256), 0, st, (bf16*)dt, (long)rows_total,
