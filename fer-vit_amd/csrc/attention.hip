@@ -396,17 +396,17 @@ __global__ __launch_bounds__(64 * NB) void attn_dkv_bf16(const bf16* __restrict_
 // the NB waves always work on NB different query blocks:
 //   S = Q K^T, dP = dO V^T (registers hold queries, lanes hold keys; once per block pair),
 //   P, dS = P o (dropout'(dP) - Dq);  dV += P_drop^T dO;  dK += dS^T Q;
-//   dQ^T(qb) += K^T dS^T: dS goes through a wave-private [key][query] LDS tile and K^T through a
-//   wave-private K image, both read by ds_read_b64_tr_b16;
-//   dQacc[qb] += that partial, after a barrier: the barrier orders the read-modify-writes of
-//   one query block by step index, so the fp32 sum order is fixed (deterministic, no atomics).
+//   dQ: wave w also owns query block w's dQ^T accumulator in registers. After the step barrier
+//   it adds K_src^T dS(w, src)^T from the dS tile (LDS, [key][query], double-buffered by step)
+//   and K image of the wave src that visited block w in this step, both read by
+//   ds_read_b64_tr_b16; the key blocks arrive in a fixed order (deterministic, no atomics).
 // S, dP, P and the dropout mask are computed once per (query block, key block) instead of once
 // in each of the dQ and dK/dV orientations of the two-kernel path.
-// LDS (NB = 7): Q + dO images 2 x 28 KB, K images 28 KB, dS tiles 14 KB, dQacc fp32 56 KB,
-// lse / Dq 1.75 KB = 155.75 KB -> one workgroup per CU.
+// LDS (NB = 7): Q + dO images 2 x 28 KB, K images 28 KB, dS tiles 2 x 14 KB, lse / Dq 1.75 KB =
+// 113.75 KB (NB = 8, N <= 256: 130 KB); 256 VGPRs -> one workgroup per CU.
 template <int NB>
 constexpr int fused_lds_bytes() {
-  return 3 * NB * 32 * 128 + NB * 2048 + NB * 32 * 64 * 4 + 2 * NB * 32 * 4;
+  return 3 * NB * 32 * 128 + 2 * NB * 2048 + 2 * NB * 32 * 4;
 }
 
 // [32][32] bf16 tile with 64-byte rows (keys x queries): B operand of the 32x32x16 MFMA with
@@ -443,16 +443,14 @@ __global__ __launch_bounds__(64 * NB) void attn_bwd_fused_bf16(const bf16* __res
   char* Qi = lds;
   char* Oi = lds + IMG;                       // dO image
   char* Kimg = lds + 2 * IMG;                 // NB x [32 keys][64 d] images
-  char* Sall = lds + 3 * IMG;                 // NB x [32 keys][32 queries] bf16 dS tiles
-  char* dqa = Sall + NB * 2048;               // dQ accumulator
-  float* lse_s = (float*)(dqa + NB * 32 * 64 * 4);
+  char* Sall = lds + 3 * IMG;                 // 2 x NB x [32 keys][32 queries] bf16 dS tiles
+  char* dqa = lds;                            // after the steps: dQ rows, fp32, over the Q / dO images
+  float* lse_s = (float*)(Sall + 2 * NB * 2048);
   float* dd_s = lse_s + NB * 32;
   const int bh = blockIdx.x, b = bh / H, h = bh - b * H, D = H * dh;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hh = lane >> 5;
   img_dma<NB>(Qi, make_rsrc(qkv), (long)b * N, ldq, h * dh, N, dh, w, lane);
   img_dma<NB>(Oi, make_rsrc(dout), (long)b * N, lddo, h * dh, N, dh, w, lane);
-  // zero the dQ accumulator
-  for (int t = threadIdx.x; t < NB * 32 * 16; t += 64 * NB) *(f32x4*)(dqa + t * 16) = f32x4{0.f, 0.f, 0.f, 0.f};
   // Dq = rowsum(dO o O): two threads per query row
   for (int t = threadIdx.x; t < NB * 64; t += 64 * NB) {
     const int qr = t >> 1, half = t & 1;
@@ -476,7 +474,6 @@ __global__ __launch_bounds__(64 * NB) void attn_bwd_fused_bf16(const bf16* __res
   const bool kval = key < N;
   bf16x8 kf[4], vf[4];
   char* Ki = Kimg + w * 4096;
-  char* Si = Sall + w * 2048;
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
     const int d0 = 16 * s + 8 * hh;
@@ -491,11 +488,13 @@ __global__ __launch_bounds__(64 * NB) void attn_bwd_fused_bf16(const bf16* __res
   const int NP = N + (N & 1);
   const bool odd = lane & 1;
   f32x16 dk[2] = {f32x16{}, f32x16{}}, dv[2] = {f32x16{}, f32x16{}};
+  f32x16 dq[2] = {f32x16{}, f32x16{}};  // dQ^T of query block w (this wave owns it), registers
   const int nsteps = (dbg & 2) ? 0 : NB;
 #pragma unroll 1
   for (int i = 0; i < nsteps; ++i) {
     int qb = w + i;
     if (qb >= NB) qb -= NB;
+    char* Si = Sall + (i & 1) * NB * 2048 + w * 2048;
     f32x16 st = {}, dp = {};
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
@@ -554,26 +553,35 @@ __global__ __launch_bounds__(64 * NB) void attn_bwd_fused_bf16(const bf16* __res
         dk[db] = mfma32(df, rd_tr(Qi, qb * 32 + 16 * s2, db * 32, lane), dk[db]);
       }
     }
-    // dQ^T(qb) partial = K^T dS^T (wave-private LDS: this wave's own writes are visible in order)
-    f32x16 dqt[2] = {f32x16{}, f32x16{}};
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      const bf16x8 sf = rd_tr64(Si, 16 * s2, lane);
-#pragma unroll
-      for (int db = 0; db < 2; ++db) dqt[db] = mfma32(rd_tr(Ki, 16 * s2, db * 32, lane), sf, dqt[db]);
-    }
-    // step barrier: the previous visitor of dQacc[qb] (wave w+1, step i-1) has finished
+    // step barrier: every wave's dS tile of this step is in Sall[i & 1] (double-buffered: the
+    // tiles of step i-1 may still be read by slow owners until they pass this barrier)
     __syncthreads();
-    const int qrow = qb * 32 + (lane & 31);
+    // dQ^T(w) += K_src^T dS(w, src)^T from the wave src that visited query block w this step;
+    // the key blocks arrive in a fixed order (w, w-1, ...): deterministic, no atomics
+    {
+      int src = w - i;
+      if (src < 0) src += NB;
+      const char* So = Sall + (i & 1) * NB * 2048 + src * 2048;
+      const char* Ko = Kimg + src * 4096;
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const bf16x8 sf = rd_tr64(So, 16 * s2, lane);
+#pragma unroll
+        for (int db = 0; db < 2; ++db) dq[db] = mfma32(rd_tr(Ko, 16 * s2, db * 32, lane), sf, dq[db]);
+      }
+    }
+  }
+  __syncthreads();  // Q / dO images no longer read: they take the dQ rows
+  {
+    const int qrow = w * 32 + (lane & 31);
 #pragma unroll
     for (int db = 0; db < 2; ++db)
 #pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        f32x4* a = (f32x4*)(dqa + dq_off(qrow, 8 * db + 2 * g4 + hh));
-        *a += f32x4{dqt[db][4 * g4], dqt[db][4 * g4 + 1], dqt[db][4 * g4 + 2], dqt[db][4 * g4 + 3]};
-      }
+      for (int g4 = 0; g4 < 4; ++g4)
+        *(f32x4*)(dqa + dq_off(qrow, 8 * db + 2 * g4 + hh)) =
+            f32x4{dq[db][4 * g4], dq[db][4 * g4 + 1], dq[db][4 * g4 + 2], dq[db][4 * g4 + 3]};
   }
-  __syncthreads();  // all dQacc updates done; Q / dO images no longer read
+  __syncthreads();
   // dQ: 16-byte row pieces, scaled
   for (int t = threadIdx.x; t < NB * 32 * 8; t += 64 * NB) {
     const int qr = t >> 3, c8 = t & 7;  // 8 d per piece
@@ -618,6 +626,7 @@ __global__ __launch_bounds__(64 * NB) void attn_bwd_fused_bf16(const bf16* __res
   }
   // dK / dV: stage each wave's 32 x 64 tiles through LDS (reusing the image area) for 16-byte
   // row stores. dk/dv[db][r]: key row = w*32 + acc_row(r, hh), d = db*32 + (lane&31).
+  __syncthreads();  // the dQ rows (same area) have been read
   bf16* stg = (bf16*)(lds + w * 8192);  // [2][32][64], inside the (now unused) Q / dO images
 #pragma unroll
   for (int db = 0; db < 2; ++db)
@@ -818,7 +827,7 @@ extern "C" int fer_attention_bwd(int dtype, const void* qkv, int64_t ld_qkv, con
   const float sl2 = scale * LOG2E;
   static const bool two_kernel = getenv("FERVIT_ATTN_BWD_2K") != nullptr;  // A/B switch
   static const int dbg = getenv("FERVIT_ATTN_DBG") ? atoi(getenv("FERVIT_ATTN_DBG")) : 0;  // timing experiments
-  if (nb <= 7 && !two_kernel) {
+  if (nb <= 8 && !two_kernel) {
 #define FER_FUSED(NBV)                                                                                       \
   case NBV:                                                                                                  \
     hipLaunchKernelGGL(attn_bwd_fused_bf16<NBV>, dim3(B * H), dim3(64 * NBV), 0, st, (const bf16*)qkv,       \
@@ -826,8 +835,9 @@ extern "C" int fer_attention_bwd(int dtype, const void* qkv, int64_t ld_qkv, con
                        (bf16*)dqkv, (long)ld_dqkv, N, H, dh, scale, sl2, drop_thresh, drop_scale, seed,      \
                        colsum ? ws : nullptr, dbg);                                                         \
     break;
-    switch (nb) {  // the fused kernel's LDS fits up to NB = 7 (N <= 224)
+    switch (nb) {  // every N <= 256
       FER_FUSED(1) FER_FUSED(2) FER_FUSED(3) FER_FUSED(4) FER_FUSED(5) FER_FUSED(6) FER_FUSED(7)
+      FER_FUSED(8)
     }
 #undef FER_FUSED
     int rc = hip_check("attention_bwd_bf16_fused");
