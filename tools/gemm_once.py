@@ -1,0 +1,25 @@
+"""Run one ViT-B GEMM a few times (PMC profiling target): GEMM_CASE=fc1|fc1_fused|wgrad."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "fer-vit_amd"))
+import torch  # noqa: E402
+
+from fervit import ops  # noqa: E402
+
+M, D, F = 256 * 197, 768, 3072
+g = torch.Generator(device="cuda").manual_seed(0)
+x = torch.randn(M, D, device="cuda", generator=g).to(torch.bfloat16)
+w = (torch.randn(F, D, device="cuda", generator=g) * 0.03).to(torch.bfloat16)
+b = torch.zeros(F, device="cuda")
+pre = torch.empty(M, F, device="cuda", dtype=torch.bfloat16)
+out = torch.empty(M, F, device="cuda", dtype=torch.bfloat16)
+case = os.environ.get("GEMM_CASE", "fc1")
+for _ in range(6):
+    if case == "fc1":
+        ops.linear_fwd(x, w, out=out)
+    else:
+        ops.linear_fwd(x, w, b, out=out, pre=pre, act="gelu", dropout=0.1, seed=7)
+torch.cuda.synchronize()
+print("done")
