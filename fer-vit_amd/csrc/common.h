@@ -88,10 +88,49 @@ FER_DEV float gelu_erf_fast(float x) {
   const float e = 1.0f - __builtin_amdgcn_rcpf(p);  // erf(|x| / sqrt 2); rcp(inf) = 0
   return 0.5f * x * (1.0f + copysignf(e, x));
 }
+// The same on two values with packed fp32 math (v_pk_fma_f32 / v_pk_mul_f32: two lanes' worth
+// per instruction); identical arithmetic per element, so bit-identical to gelu_erf_fast.
+typedef __attribute__((ext_vector_type(2))) float f32x2;
+// A packed-math constant materialised where it is used: without the barrier the compiler hoists
+// every such constant into an SGPR pair for the whole kernel, and the GEMM's main loop then
+// spills SGPRs.
+FER_DEV f32x2 kpk(float c) {
+  asm volatile("" : "+s"(c));
+  return f32x2(c);
+}
+FER_DEV f32x2 gelu_erf_fast2(f32x2 x) {
+  const f32x2 z = __builtin_elementwise_abs(x) * 0.70710678118654752f;
+  f32x2 p = __builtin_elementwise_fma(kpk(4.30638e-5f), z, kpk(2.765672e-4f));
+  p = __builtin_elementwise_fma(p, z, kpk(1.520143e-4f));
+  p = __builtin_elementwise_fma(p, z, kpk(9.2705272e-3f));
+  p = __builtin_elementwise_fma(p, z, kpk(4.22820123e-2f));
+  p = __builtin_elementwise_fma(p, z, kpk(7.05230784e-2f));
+  p = __builtin_elementwise_fma(p, z, f32x2(1.0f));
+  p *= p;
+  p *= p;
+  p *= p;
+  p *= p;
+  const f32x2 e = 1.0f - f32x2{__builtin_amdgcn_rcpf(p[0]), __builtin_amdgcn_rcpf(p[1])};
+  return 0.5f * x * (1.0f + __builtin_elementwise_copysign(e, x));
+}
 FER_DEV float gelu_erf_grad(float x) {
   const float e = __expf(-0.5f * x * x);
   const float cdf = 0.5f * (1.0f + fast_erf_from_exp(x * 0.70710678118654752f, e));
   return fmaf(x * 0.39894228040143268f, e, cdf);
+}
+FER_DEV f32x2 gelu_erf_grad2(f32x2 x) {  // packed gelu_erf_grad, same arithmetic per element
+  const f32x2 h = -0.5f * x * x;
+  const f32x2 e = f32x2{__expf(h[0]), __expf(h[1])};
+  const f32x2 z = x * 0.70710678118654752f;
+  const f32x2 d = __builtin_elementwise_fma(kpk(0.3275911f), __builtin_elementwise_abs(z), f32x2(1.0f));
+  const f32x2 t = f32x2{__builtin_amdgcn_rcpf(d[0]), __builtin_amdgcn_rcpf(d[1])};
+  f32x2 y = __builtin_elementwise_fma(kpk(1.061405429f), t, kpk(-1.453152027f));
+  y = __builtin_elementwise_fma(y, t, kpk(1.421413741f));
+  y = __builtin_elementwise_fma(y, t, kpk(-0.284496736f));
+  y = __builtin_elementwise_fma(y, t, kpk(0.254829592f));
+  const f32x2 r = 1.0f - y * t * e;
+  const f32x2 cdf = 0.5f * (1.0f + __builtin_elementwise_copysign(r, z));
+  return __builtin_elementwise_fma(x * 0.39894228040143268f, e, cdf);
 }
 FER_DEV float act_fwd(int act, float x) {
   return act == FER_ACT_GELU ? gelu_erf(x) : (act == FER_ACT_RELU ? fmaxf(x, 0.f) : x);

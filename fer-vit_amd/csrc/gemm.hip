@@ -46,11 +46,10 @@ FER_DEV void epi8_bf16(const EpiArgs& e, long m, long n, f32x4& v0, f32x4& v1, f
   v1 = v1 * e.alpha + b1;
   if (e.pre) *(bf16x8*)((bf16*)e.pre + m * e.ldp + n) = pack8(v0, v1);
   if (e.act == FER_ACT_GELU) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      v0[r] = gelu_erf_fast(v0[r]);
-      v1[r] = gelu_erf_fast(v1[r]);
-    }
+    v0.xy = gelu_erf_fast2(v0.xy);
+    v0.zw = gelu_erf_fast2(v0.zw);
+    v1.xy = gelu_erf_fast2(v1.xy);
+    v1.zw = gelu_erf_fast2(v1.zw);
   } else if (e.act == FER_ACT_RELU) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -70,10 +69,17 @@ FER_DEV void epi8_bf16(const EpiArgs& e, long m, long n, f32x4& v0, f32x4& v1, f
   if (e.aux) {
     const bf16x8 a = e.res ? *(const bf16x8*)((const bf16*)e.aux + m * e.ldx + n) : x;
     const f32x4 a0 = lo4(a), a1 = hi4(a);
+    if (e.aux_act == FER_ACT_GELU) {
+      v0.xy *= gelu_erf_grad2(a0.xy);
+      v0.zw *= gelu_erf_grad2(a0.zw);
+      v1.xy *= gelu_erf_grad2(a1.xy);
+      v1.zw *= gelu_erf_grad2(a1.zw);
+    } else {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      v0[r] *= act_grad(e.aux_act, a0[r]);
-      v1[r] *= act_grad(e.aux_act, a1[r]);
+      for (int r = 0; r < 4; ++r) {
+        v0[r] *= act_grad(e.aux_act, a0[r]);
+        v1[r] *= act_grad(e.aux_act, a1[r]);
+      }
     }
   }
   if (e.res) {
