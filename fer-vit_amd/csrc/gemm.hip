@@ -706,6 +706,29 @@ struct UnitPlan {
   }
 };
 
+#ifdef FER_GEMM_STAMPS
+// Diagnostic build only (cdna_hip_programming.md §7 in-kernel stamps): wave 0 and wave 4 of
+// workgroup 0 record s_memtime at the phase boundaries of their second tile into LDS, dumped to
+// g_stamps after the main loop. Never built into libfervit.so.
+__device__ unsigned long long g_stamps[2][4 + 16 * 4 * 4];
+FER_DEV unsigned long long stamp_now() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+#define FER_STAMP(i)                                              \
+  do {                                                            \
+    if (st_on) {                                                  \
+      const unsigned long long t_ = stamp_now();                  \
+      if (lane == 0) st_l[st_w * (4 + 256) + (i)] = t_;           \
+    }                                                             \
+  } while (0)
+#else
+#define FER_STAMP(i) do {} while (0)
+#endif
+
 template <bool AKC, bool BKC, int MT>
 FER_DEV void tile_8ph(const GemmArgs& g, const EpiArgs& e, int bid, char* smem) {
   typedef typename Acc<MT>::T AccT;
@@ -720,6 +743,12 @@ FER_DEV void tile_8ph(const GemmArgs& g, const EpiArgs& e, int bid, char* smem) 
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
+#ifdef FER_GEMM_STAMPS
+  __shared__ unsigned long long st_l[2 * (4 + 256)];
+  const bool st_on = blockIdx.x == 0 && blockIdx.y == 0 && bid == (int)gridDim.x && (wave & 3) == 0;
+  const int st_w = wave >> 2;
+#endif
+  FER_STAMP(0);
 
   int tm, tn;
   tile_of(bid, g.tiles_m, g.tiles_n, tm, tn);
@@ -764,11 +793,14 @@ FER_DEV void tile_8ph(const GemmArgs& g, const EpiArgs& e, int bid, char* smem) 
     if (wr) __builtin_amdgcn_s_barrier();  // stagger: waves 4-7 one barrier behind
     asm volatile("" ::: "memory");
   }
+  FER_STAMP(1);
 
   for (int T = 0; T < nk; ++T) {
     const bool n1 = T + 1 < nk, n2 = T + 2 < nk;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
+      const int st_i = 4 + (T * 4 + q) * 4;
+      if (T < 16) FER_STAMP(st_i);
       // ---- load segment
       if (q < 2) {
         const char* ua = unit(T, q);
@@ -791,8 +823,10 @@ FER_DEV void tile_8ph(const GemmArgs& g, const EpiArgs& e, int bid, char* smem) 
       } else {
         if (n2) { iA0(T + 2); wait_vm<6>(); } else if (n1) { wait_vm<4>(); }
       }
+      if (T < 16) FER_STAMP(st_i + 1);
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
+      if (T < 16) FER_STAMP(st_i + 2);
       // ---- MFMA segment: quadrant (qm, qn) for q = 0..3 -> (0,0) (1,1) (0,1) (1,0)
       constexpr int dummy = 0;
       (void)dummy;
@@ -808,17 +842,26 @@ FER_DEV void tile_8ph(const GemmArgs& g, const EpiArgs& e, int bid, char* smem) 
             acc[qn * QI + i][qm * QJ + j] = mfma<MT>(fb[qn][kk][i], fa[qm][kk][j], acc[qn * QI + i][qm * QJ + j]);
       __builtin_amdgcn_s_setprio(0);
       __builtin_amdgcn_sched_barrier(0);
+      if (T < 16) FER_STAMP(st_i + 3);
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
     }
   }
   if (nk > 0 && !wr) __builtin_amdgcn_s_barrier();  // waves 0-3 catch up with the stagger
+  FER_STAMP(2);
   if (g.dbg & 4) {  // timing experiment: no epilogue (keep the MFMAs alive)
     if (acc[0][0][0] == 12345.f) g.ws[0] = 1.f;
     return;
   }
   static_assert(64 * (256 + 4) * 4 <= 2 * BUF, "epilogue staging (2 chunks per half) must fit");
   tile_epilogue<256, 256, 2, 4, MT, 2, 2 * BUF>(g, e, acc, smem, m0, n0, ks, wr, wc, lane);
+  FER_STAMP(3);
+#ifdef FER_GEMM_STAMPS
+  if (st_on) {
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    for (int i = lane; i < 4 + 256; i += 64) g_stamps[st_w][i] = st_l[st_w * (4 + 256) + i];
+  }
+#endif
 }
 
 // Persistent launch (one workgroup per CU, tiles bid, bid + grid, ...: the XCD-aware tile order
@@ -931,6 +974,12 @@ static int launch_8ph(GemmArgs g, const EpiArgs& e, hipStream_t st) {
   hipLaunchKernelGGL((gemm_8ph_kernel<AKC, BKC, MT>), grid, dim3(512), 0, st, g, e);
   return 0;
 }
+
+#ifdef FER_GEMM_STAMPS
+extern "C" int fer_debug_gemm_stamps(unsigned long long* host, int n) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * n) == hipSuccess ? 0 : 1;
+}
+#endif
 
 static int g_forced_cfg = -2;  // -2: read FERVIT_GEMM_CFG once; -1: automatic
 
