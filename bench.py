@@ -1,20 +1,31 @@
 """Headline benchmark: training images/s of ViT-B/16 (224x224 RGB, per-GPU bs=256,
 dropout 0.1, label-smoothed CE, AdamW) — BASELINE.json configs[2] — on 1..8 MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config vit_base_224|latent_vit|image_vit_48]
-    (N>1: torch.distributed.run, one rank per GPU, RCCL all-reduce over xGMI)
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config vit_base_224|latent_vit|image_vit_48|...]
+
+--gpus N > 1 without a torch.distributed environment: this process starts
+`python -m torch.distributed.run --nproc-per-node N ... bench.py` as a CHILD (it never touches
+the GPU itself) and relays rank 0's JSON line; under torch.distributed.run (the driver's
+launch) every rank runs the step on its own GPU, RCCL all-reduce over xGMI.
 
 A step = zero_grad -> forward -> CE -> backward (bucketed all-reduce overlapped when N>1)
--> fused AdamW, on synthetic data already resident in HBM. Rank 0 prints one JSON line.
+-> fused AdamW, on synthetic data already resident in HBM. W untimed warm-up steps, then K
+steps bracketed by barrier + synchronize (value = all ranks' images / the max over ranks of
+that time); one HIP event per step boundary gives the per-step median / p10 / p90.
 
-roofline: the dominant kernel is the bf16 MFMA GEMM of the FFN up-projection
-(linear1, [B*197 x 768] x [3072 x 768]^T + bias + GELU + dropout epilogue). Its launches
-inside the timed region are bracketed by HIP events on the launch stream; achieved =
-2*M*N*K / mean launch time vs the dense bf16 MFMA peak (MI355X_MICROARCH.md: 256 CU x 4
-SIMD x 1024 FLOP/clk x 2.4 GHz = 2516.6 TFLOP/s). `step_mfma_frac` is the whole step's
-algorithmic GEMM+attention FLOPs (105.38 GFLOP/img fwd+bwd) / step time / peak.
+roofline: the dominant kernel is `gemm_8ph_kernel`, the bf16 MFMA GEMM of every forward and
+input-gradient linear (QKV, out-proj, fc1, fc2, patch embed; ~55 % of the step). Its launches
+are timed in a separate PROBE phase after the timed region (HIP events on the launch stream
+around each launch, so the timed region carries no probe events): achieved = sum over one
+step's 8-phase launches of 2*M*N*K / sum of their durations, vs the dense bf16 MFMA peak
+(MI355X_MICROARCH.md: 256 CU x 4 SIMD x 1024 FLOP/clk x 2.4 GHz = 2516.6 TFLOP/s).
+`traffic` = HBM bytes per launch of that kernel from rocprofv3 PMC passes (FETCH_SIZE,
+WRITE_SIZE; one counter per pass, child processes run before this process touches the GPU).
+`step_mfma_frac` is the whole step's algorithmic GEMM+attention FLOPs (SURVEY §8d:
+105.38 GFLOP/img fwd+bwd) / step time / peak.
 cpu_baseline: the CPU oracle (oracle/vit_oracle.py, same model, fp32, dropout 0.1, AdamW)
-timed on the host cores for a bounded sample (rank 0, N=1 only).
+timed on the host cores for a bounded sample (rank 0, N=1 only); cpu_baseline_cfg1 the same
+for BASELINE configs[0] (48 px ImageViT d6/h8, bs=64, the reference's CPU-runnable case).
 """
 from __future__ import annotations
 
@@ -97,36 +108,73 @@ def build(cfg_name, device):
     return m, opt, CrossEntropyLoss(label_smoothing=ls), B, shape, desc
 
 
-class GemmProbe:
-    """HIP events around the launches of one GEMM signature, on the launch stream."""
+def is_8ph(d) -> bool:
+    """The launches csrc/gemm.hip sends to gemm_8ph_kernel (automatic configuration): bf16,
+    both operands K-contiguous, a grid of >= 256 256x256 tiles (or K >= 8192)."""
+    t256 = -(-d.M // 256) * -(-d.N // 256)
+    return d.dtype == 0 and bool(d.a_kc) and bool(d.b_kc) and (d.K >= 8192 or t256 >= 256)
 
-    def __init__(self, M, N, K):
-        self.sig = (M, N, K)
-        self.events = []
+
+def gemm_algo_bytes(d, e) -> int:
+    """Minimum HBM bytes of one GEMM launch: A and B read once, every epilogue operand read once
+    (bias, res, aux rows), the output (and pre-activation) written once, at storage dtypes."""
+    out_b = 4 if e.c_f32 else 2
+    n = 2 * (d.M * d.K + d.N * d.K) + d.M * d.N * out_b * (2 if e.accumulate else 1)
+    if e.bias:
+        n += 4 * d.N
+    for ptr_ in (e.pre, e.res, e.aux):
+        if ptr_:
+            n += 2 * d.M * d.N
+    return n
+
+
+class GemmProbe:
+    """HIP events around every gemm_8ph launch, on the launch stream (probe phase only)."""
+
+    def __init__(self):
+        self.rec = []
         self.on = False
 
-    def __call__(self, desc, launch):
-        if not self.on or (desc.M, desc.N, desc.K) != self.sig or not (desc.a_kc and desc.b_kc):
+    def __call__(self, d, e, launch):
+        if not self.on or not is_8ph(d):
             return launch()
         s = torch.cuda.current_stream()
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record(s)
         r = launch()
         b.record(s)
-        self.events.append((a, b))
+        parts = [n for n, on in (("bias", e.bias), ("gelu" if e.act == 1 else "relu", e.act), ("drop", e.drop_thresh),
+                                 ("pre", e.pre), ("act'", e.aux), ("res", e.res), ("colsum", e.colsum)) if on]
+        kind = "epi:" + ("+".join(parts) or "none")
+        self.rec.append(((d.M, d.N, d.K), kind, 2.0 * d.M * d.N * d.K, gemm_algo_bytes(d, e), a, b))
         return r
 
-    def mean_ms(self):
-        ts = [a.elapsed_time(b) for a, b in self.events]
-        return sum(ts) / max(1, len(ts)), len(ts)
+    def summary(self, steps):
+        tot_ms = sum(a.elapsed_time(b) for *_, a, b in self.rec)
+        flops = sum(r[2] for r in self.rec)
+        nbytes = sum(r[3] for r in self.rec)
+        n = len(self.rec)
+        shapes = {}
+        for (mnk, kind, fl, _, a, b) in self.rec:
+            k = f"{mnk[0]}x{mnk[1]}x{mnk[2]} {kind}"
+            c = shapes.setdefault(k, [0, 0.0, fl])
+            c[0] += 1
+            c[1] += a.elapsed_time(b)
+        per_shape = {k: {"launches_per_step": v[0] // max(1, steps), "mean_us": round(1e3 * v[1] / v[0], 1),
+                         "tflops": round(v[2] / (v[1] / v[0] / 1e3) / 1e12, 1)} for k, v in shapes.items()}
+        return {"launches": n, "launches_per_step": n // max(1, steps), "mean_launch_ms": tot_ms / max(1, n),
+                "flop_per_launch": flops / max(1, n), "algo_bytes_per_launch": nbytes / max(1, n),
+                "ms_per_step": tot_ms / max(1, steps), "per_shape": per_shape}
 
 
-def pmc_traffic(timeout_s=120):
-    """HBM bytes per launch of the roofline kernel from rocprofv3 PMC counters, one counter per
-    pass (MI355X_MICROARCH.md: FETCH_SIZE / WRITE_SIZE in KiB; on gfx950 FETCH_SIZE reads half the
-    bytes of a 16 B/lane streaming read -- the GEMM's LDS-DMA operand loads -- so it is doubled;
-    WRITE_SIZE is exact for 16 B/lane stores). Runs tools/traffic_probe.py as a CHILD process under
-    rocprofv3 before this process touches the GPU. Returns (bytes, detail) or (None, reason)."""
+def pmc_traffic(timeout_s=240):
+    """HBM bytes per launch of the roofline kernel (gemm_8ph_kernel) from rocprofv3 PMC counters,
+    one counter per pass (MI355X_MICROARCH.md: FETCH_SIZE / WRITE_SIZE in KiB; on gfx950
+    FETCH_SIZE reads half the bytes of a 16 B/lane streaming read -- the GEMM's LDS-DMA operand
+    loads -- so it is doubled; WRITE_SIZE is exact for 16 B/lane stores). Runs
+    tools/traffic_probe.py (ViT-B/16 bs=256 train steps) as a CHILD process under rocprofv3
+    before this process touches the GPU; averages every gemm_8ph dispatch of the run.
+    Returns (bytes, detail) or (None, reason)."""
     import csv
     import glob
     import shutil
@@ -152,22 +200,27 @@ def pmc_traffic(timeout_s=120):
         per = []
         with open(files[0]) as f:
             for row in csv.DictReader(f):
-                if "gemm" in row.get("Kernel_Name", "") and row.get("Counter_Name", "") == ctr:
+                if "gemm_8ph" in row.get("Kernel_Name", "") and row.get("Counter_Name", "") == ctr:
                     per.append(float(row["Counter_Value"]))
         shutil.rmtree(d, ignore_errors=True)
         if not per:
-            return None, f"{ctr}: no gemm dispatch in the counter CSV"
-        per.sort()
-        vals[ctr] = per[len(per) // 2]  # median over the probe's launches (KiB)
-    read_b = 2.0 * vals["FETCH_SIZE"] * 1024
-    write_b = vals["WRITE_SIZE"] * 1024
-    return read_b + write_b, {"read_bytes": read_b, "write_bytes": write_b, "fetch_size_kib": vals["FETCH_SIZE"],
-                              "write_size_kib": vals["WRITE_SIZE"], "method": "rocprofv3 --pmc, one counter per "
-                              "pass, median over 6 launches; read = 2*FETCH_SIZE (gfx950 16 B/lane correction)"}
+            return None, f"{ctr}: no gemm_8ph dispatch in the counter CSV"
+        vals[ctr] = (sum(per) / len(per), len(per))  # mean over the probe's launches (KiB)
+    read_b = 2.0 * vals["FETCH_SIZE"][0] * 1024
+    write_b = vals["WRITE_SIZE"][0] * 1024
+    return read_b + write_b, {"read_bytes": round(read_b), "write_bytes": round(write_b),
+                              "fetch_size_kib": vals["FETCH_SIZE"][0], "write_size_kib": vals["WRITE_SIZE"][0],
+                              "dispatches": vals["FETCH_SIZE"][1],
+                              "method": "rocprofv3 --pmc, one counter per pass, mean over every gemm_8ph dispatch "
+                                        "of 2 ViT-B/16 bs=256 train steps (tools/traffic_probe.py); read = "
+                                        "2*FETCH_SIZE (gfx950 16 B/lane correction)"}
 
 
-def cpu_baseline(cfg_name, budget_s=20.0):
-    """Oracle train step (fp32, torch CPU ops) on a bounded sample of the workload."""
+def cpu_baseline(cfg_name, budget_s=12.0, bs=None):
+    """Oracle train step (fp32, torch CPU ops: oracle/vit_oracle.py, zero_grad -> fwd (dropout
+    0.1) -> CE(ls 0.1) -> bwd -> AdamW as `train/train_image_vit.py:117-130`) on a bounded
+    sample of the workload: `bs` images per step (default: the config's batch for small
+    models, 2 for ViT-B), up to 20 timed steps within about budget_s."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import vit_oracle as O
 
@@ -190,19 +243,20 @@ def cpu_baseline(cfg_name, budget_s=20.0):
          "norm.bias": torch.zeros(D), "head.weight": torch.randn(7, D, generator=g) * 0.02, "head.bias": torch.zeros(7)}
     for i in range(L):
         pre = f"transformer.layers.{i}."
-        for k, s in (("self_attn.in_proj_weight", (3 * D, D)), ("self_attn.out_proj.weight", (D, D)),
-                     ("linear1.weight", (F, D)), ("linear2.weight", (D, F))):
-            p[pre + k] = torch.randn(*s, generator=g) * 0.02
-        for k, s in (("self_attn.in_proj_bias", 3 * D), ("self_attn.out_proj.bias", D), ("linear1.bias", F),
-                     ("linear2.bias", D), ("norm1.bias", D), ("norm2.bias", D)):
-            p[pre + k] = torch.zeros(s)
+        for k, s_ in (("self_attn.in_proj_weight", (3 * D, D)), ("self_attn.out_proj.weight", (D, D)),
+                      ("linear1.weight", (F, D)), ("linear2.weight", (D, F))):
+            p[pre + k] = torch.randn(*s_, generator=g) * 0.02
+        for k, s_ in (("self_attn.in_proj_bias", 3 * D), ("self_attn.out_proj.bias", D), ("linear1.bias", F),
+                      ("linear2.bias", D), ("norm1.bias", D), ("norm2.bias", D)):
+            p[pre + k] = torch.zeros(s_)
         p[pre + "norm1.weight"] = torch.ones(D)
         p[pre + "norm2.weight"] = torch.ones(D)
     for t in p.values():
         t.requires_grad_(True)
     m = {k: torch.zeros_like(v) for k, v in p.items()}
     v2 = {k: torch.zeros_like(v) for k, v in p.items()}
-    bs = 2 if D >= 768 else 16
+    if bs is None:
+        bs = 2 if D >= 768 else B
     x = torch.randn(bs, *shape, generator=g)
     y = torch.randint(0, 7, (bs,), generator=g)
     step = [0]
@@ -228,34 +282,86 @@ def cpu_baseline(cfg_name, budget_s=20.0):
             break
     times.sort()
     med = times[len(times) // 2]
-    return {"value": bs / med, "unit": "images/s", "cores": threads, "kind": "port",
-            "sample": f"oracle ViT train step (fwd+bwd+AdamW, fp32, dropout 0.1) at bs={bs}, "
+    return {"value": round(bs / med, 3), "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"{cfg_name}: oracle train step (fwd+bwd+AdamW, fp32, dropout 0.1, CE ls 0.1) at bs={bs}, "
                       f"{len(times)} timed steps, median {med * 1e3:.0f} ms/step, torch {torch.__version__}"}
+
+
+def spawn_ranks(args) -> int:
+    """--gpus N > 1 outside torch.distributed: run this script under torch.distributed.run as a
+    child process (this process never initialises the GPU) and relay its output."""
+    import socket
+    import subprocess
+
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "4")
+    r = subprocess.run(cmd, env=env)
+    return r.returncode
+
+
+def percentile(xs, q):
+    xs = sorted(xs)
+    if not xs:
+        return None
+    i = min(len(xs) - 1, max(0, int(round(q * (len(xs) - 1)))))
+    return xs[i]
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="vit_base_224", choices=list(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC traffic passes")
+    ap.add_argument("--probe-steps", type=int, default=2, help="steps of the (untimed) roofline probe phase")
     ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
                     help="replay the whole step as a HIP graph (auto: on for the launch-bound small configs)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launch plumbing only (gloo, CPU): ranks rendezvous, barrier, rank 0 prints the JSON line")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    traffic, traffic_detail = None, "not measured (N>1 or --no-traffic)"
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.dry_run:
+        if world > 1:
+            dist.init_process_group("gloo")
+            dist.barrier()
+            seen = dist.get_world_size()
+            dist.destroy_process_group()
+        else:
+            seen = 1
+        if rank == 0:
+            print(json.dumps({"metric": METRIC, "value": None, "unit": "images/s", "n_gpus": world,
+                              "ranks_seen": seen, "dry_run": True}), flush=True)
+        return
+
+    traffic, traffic_detail = None, "not measured (N>1, --no-traffic or not the ViT-B/16 config)"
     if world == 1 and not args.no_traffic and args.config == "vit_base_224":
         # child rocprofv3 passes first: this process has not initialised the GPU yet
         traffic, traffic_detail = pmc_traffic()
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
+    rccl = None
     if world > 1:
         dist.init_process_group("nccl", device_id=device)
+        try:
+            v = torch.cuda.nccl.version()
+            rccl = ".".join(str(x) for x in v) if isinstance(v, tuple) else str(v)
+        except Exception:  # noqa: BLE001
+            rccl = "unknown"
 
     import fervit
     from fervit import ops
@@ -286,7 +392,7 @@ def main():
         trunk = gemm_flops_per_img(D, L, F, N) // 3
         adapters = L * 2 * N * (2 * D * 64)
         flops_img = 2 * trunk + 3 * (adapters + 2 * 18 * 512 * D + 2 * D * 7)
-    probe = GemmProbe(B * N, F, D)
+    probe = GemmProbe()
     ops.LAUNCH_PROBE = probe
 
     def step():
@@ -297,68 +403,81 @@ def main():
         return loss
 
     use_graph = args.graph == "on" or (args.graph == "auto" and args.config != "vit_base_224" and world == 1)
+    for _ in range(args.warmup):
+        step()
     if use_graph:
-        # the roofline kernel is timed in eager warm-up steps (HIP events cannot bracket single
-        # launches inside a replayed graph); the timed region replays the captured step
         from fervit.graph import StepGraph
 
-        probe.on = True
-        for _ in range(args.warmup):
-            step()
-        probe.on = False
         graph = StepGraph(step, opt, warmup=1).capture()
         run = graph.replay
     else:
-        for _ in range(args.warmup):
-            step()
         run = step
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    probe.on = not use_graph
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    ev[0].record()
+    for i in range(args.steps):
         loss = run()
+        ev[i + 1].record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
-    probe.on = False
     if world > 1:
         t = torch.tensor([el], device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = t.item()
-    gemm_ms, nlaunch = probe.mean_ms()
+    step_ms = [ev[i].elapsed_time(ev[i + 1]) for i in range(args.steps)]
+    lossv = loss.item()
+    # probe phase (untimed): HIP events around every gemm_8ph launch of a few eager steps
+    if use_graph:
+        graph.release()
+    probe.on = True
+    for _ in range(args.probe_steps):
+        step()
+    torch.cuda.synchronize()
+    probe.on = False
+    ps = probe.summary(args.probe_steps)
     ms = el / args.steps * 1e3
     imgs = world * B * args.steps / el
     step_tflops = flops_img * B / (ms / 1e3) / 1e12
-    gemm_flop = 2.0 * B * N * F * D
-    # bytes the fc1 launch must move at minimum: X [BN x D] + W1 [F x D] read, pre + out [BN x F] written (bf16)
-    algo_bytes = 2 * (B * N * D + F * D + 2 * B * N * F)
-    achieved = gemm_flop / (gemm_ms / 1e3) / 1e12
-    lossv = loss.item()
+    achieved = ps["flop_per_launch"] / (ps["mean_launch_ms"] / 1e3) / 1e12 if ps["launches"] else 0.0
     if rank == 0:
-        cpu = None
+        cpu = cpu1 = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(args.config)
+            if args.config == "vit_base_224":
+                cpu1 = cpu_baseline("image_vit_48", bs=64)
         out = {
             "metric": METRIC, "value": round(imgs, 2), "unit": "images/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "bf16", "data": "synthetic (N(0,1) inputs, uniform labels), random init",
             "config": {"workload": desc, "per_gpu_batch": B, "global_batch": B * world, "tokens": N,
                        "parallelism": f"dp{world}"},
-            "roofline": {"bound": "mfma", "kernel": f"gemm_bf16 linear1 fwd [{B * N}x{D}]x[{F}x{D}]^T",
+            "step_ms_median": round(percentile(step_ms, 0.5), 3), "step_ms_p10": round(percentile(step_ms, 0.1), 3),
+            "step_ms_p90": round(percentile(step_ms, 0.9), 3),
+            "roofline": {"bound": "mfma", "kernel": "gemm_8ph_kernel (bf16 MFMA; every fwd + dgrad linear and the "
+                                                    "patch embed, fused epilogues)",
                          "achieved": round(achieved, 1), "peak": round(PEAK_BF16_TFLOPS, 1), "unit": "TFLOP/s",
                          "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
                          "traffic": None if traffic is None else round(traffic),
                          "traffic_detail": traffic_detail,
-                         "algorithmic_bytes": algo_bytes,
-                         "launches_timed": nlaunch, "mean_launch_ms": round(gemm_ms, 4)},
+                         "algorithmic_bytes": round(ps["algo_bytes_per_launch"]),
+                         "flop_per_launch": round(ps["flop_per_launch"]),
+                         "launches_per_step": ps["launches_per_step"],
+                         "mean_launch_ms": round(ps["mean_launch_ms"], 4),
+                         "kernel_ms_per_step": round(ps["ms_per_step"], 3),
+                         "per_shape": ps["per_shape"]},
             "launch": "hipGraph replay of the whole step" if use_graph else "eager (one host launch per kernel)",
             "step_mfma_frac": round(step_tflops / PEAK_BF16_TFLOPS, 4),
             "step_tflops": round(step_tflops, 1),
             "final_loss": round(lossv, 4),
+            "ranks_seen": dist.get_world_size() if world > 1 else 1,
+            "rccl": rccl,
             "cpu_baseline": cpu,
+            "cpu_baseline_cfg1": cpu1,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

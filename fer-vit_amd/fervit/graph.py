@@ -61,5 +61,8 @@ class StepGraph:
         return self.out
 
     def release(self) -> None:
+        """Back to eager stepping: the optimizer folds the replay count into its host step
+        counts (so checkpoints and later eager steps keep the right bias correction)."""
         check(lib().fer_set_step_counter(None), "set_step_counter")
         self.graph = None
+        self.opt.unfreeze()

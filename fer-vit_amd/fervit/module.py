@@ -52,6 +52,9 @@ class FerModule(nn.Module):
         owner = self._fer_owner() if self._fer_owner is not None else None
         if owner is not None and owner._fer_flat is not None:
             return owner._fer_flat
+        if self._fer_flat is not None:
+            self._fer_flat.begin_pass()
+            return self._fer_flat
         if self._fer_flat is None:
             params = self.fer_param_order()
             if not params:

@@ -16,7 +16,7 @@ from ._lib import Epilogue, GemmDesc, check, lib
 
 ACT = {"none": 0, "gelu": 1, "relu": 2}
 
-# Optional callable(desc, launch) used by bench.py to bracket launches with HIP events.
+# Optional callable(desc, epilogue, launch) used by bench.py to bracket launches with HIP events.
 LAUNCH_PROBE = None
 
 
@@ -122,7 +122,7 @@ def gemm(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, *, a_kc: bool = Tr
     e.colsum = ptr(colsum)
     e.colsum_accumulate = int(colsum_accumulate)
     if LAUNCH_PROBE is not None:
-        LAUNCH_PROBE(d, lambda: check(lib().fer_gemm(C_ref(d), C_ref(e), stream()), "gemm"))
+        LAUNCH_PROBE(d, e, lambda: check(lib().fer_gemm(C_ref(d), C_ref(e), stream()), "gemm"))
     else:
         check(lib().fer_gemm(C_ref(d), C_ref(e), stream()), "gemm")
     return out

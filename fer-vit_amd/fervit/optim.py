@@ -97,6 +97,21 @@ class FusedAdamW(torch.optim.Optimizer):
         self._frozen = (self._upload(segs, flat), len(segs), maxn)
         self._step_counter = counter
 
+    def unfreeze(self) -> None:
+        """Leave graph mode (StepGraph.release): the replays' device step count is folded into
+        every parameter's host 'step', so state_dict() and later eager steps continue the bias
+        correction where the replays left it."""
+        if self._step_counter is not None:
+            n = int(self._step_counter.item())
+            if n:
+                for g in self.param_groups:
+                    for p in g["params"]:
+                        st = self.state.get(p)
+                        if st is not None and "step" in st:
+                            st["step"] = st["step"] + n
+        self._frozen = None
+        self._step_counter = None
+
     def _segments(self, flat, bump: bool):
         segs = []
         maxn = 0
@@ -138,10 +153,9 @@ class FusedAdamW(torch.optim.Optimizer):
             half = flat.bf16()
             check(lib().fer_adamw(flat.data.data_ptr(), flat.grad.data_ptr(), self._m.data_ptr(),
                                   self._v.data_ptr(), half.data_ptr(), dev.data_ptr(), nseg, maxn,
-                                  float(self.grad_scale), ops.ptr(self.clip_coef),
+                                  float(self.grad_scale), ops.ptr(self._take_clip()),
                                   self._step_counter.data_ptr(), ops.stream()), "adamw")
             flat.mark_half_fresh()
-            self.clip_coef = None
             return loss
         segs, maxn = self._segments(flat, bump=True)
         if not segs:
@@ -151,20 +165,43 @@ class FusedAdamW(torch.optim.Optimizer):
         half = flat.bf16()
         check(lib().fer_adamw(flat.data.data_ptr(), flat.grad.data_ptr(), self._m.data_ptr(), self._v.data_ptr(),
                               half.data_ptr(), dev.data_ptr(), len(segs), maxn, float(self.grad_scale),
-                              ops.ptr(self.clip_coef), None, ops.stream()), "adamw")
+                              ops.ptr(self._take_clip()), None, ops.stream()), "adamw")
         flat.mark_half_fresh()
-        self.clip_coef = None
         return loss
 
+    def _take_clip(self) -> Optional[torch.Tensor]:
+        """The pending clip coefficient (set by clip_grad_norm_ through `optimizer=` or left on
+        the model), consumed by this step."""
+        coef = self.clip_coef
+        if coef is None and self.model is not None:
+            coef = getattr(self.model, "_fer_clip_coef", None)
+        self.clip_coef = None
+        if self.model is not None and hasattr(self.model, "_fer_clip_coef"):
+            self.model._fer_clip_coef = None
+        return coef
 
-def clip_grad_norm_(model, max_norm: float, sq_scale: float = 1.0) -> torch.Tensor:
-    """Device-side clip_grad_norm_ over the model's flat grad buffer: returns the total
-    norm (device scalar) and leaves the clip coefficient for FusedAdamW in
-    `model._fer_clip_coef` (no host synchronisation)."""
+
+def clip_grad_norm_(model, max_norm: float, sq_scale: float = 1.0, optimizer: Optional[FusedAdamW] = None
+                    ) -> torch.Tensor:
+    """torch.nn.utils.clip_grad_norm_ (`train/train_latent_vit_v2.py:133`) on the model's flat
+    grad buffer without a host synchronisation: total = ||g||_2 over every gradient, coef =
+    min(1, max_norm / (total + 1e-6)). The gradients are not rescaled here: the coefficient is
+    handed to the fused optimizer (`optimizer.clip_coef`, and `model._fer_clip_coef` for a
+    FusedAdamW bound to this model), whose next step multiplies every gradient by it -- the
+    same arithmetic as torch's in-place `g *= coef` followed by AdamW. Returns the total norm
+    (device scalar), as torch does. Parameters without a gradient hold zeros in the flat buffer
+    (it starts zeroed and only gradient writes touch it), so they add nothing, like torch's
+    skip of `p.grad is None`."""
     flat = model.fer_flat()
     out = torch.empty(2, dtype=torch.float32, device=flat.grad.device)
     ws = ops.WS.get(4 * 4096, flat.grad.device, slot=3)
     check(lib().fer_sumsq(flat.grad.data_ptr(), flat.numel, out.data_ptr(), ws.data_ptr(), ws.numel() * 4,
                           ops.stream()), "sumsq")
     check(lib().fer_clip_coef(out.data_ptr(), sq_scale, float(max_norm), out[1:].data_ptr(), ops.stream()), "clip")
-    return out
+    coef = out[1:]
+    model._fer_clip_coef = coef
+    if optimizer is not None:
+        optimizer.clip_coef = coef
+    if sq_scale == 1.0:
+        return out[0].sqrt()
+    return (out[0] * sq_scale).sqrt()

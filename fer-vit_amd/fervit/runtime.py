@@ -72,6 +72,7 @@ class FlatParams:
         self.grad = torch.zeros(self.numel, dtype=torch.float32, device=dev)
         self.half: Optional[torch.Tensor] = None
         self.half_version = -1
+        self._checked = False  # version signature already compared during this forward pass
         self.half_t: Optional[torch.Tensor] = None  # transposed bf16 copies of the 2-D params
         self._tsegs: Optional[torch.Tensor] = None
         self._ttiles = 0
@@ -98,12 +99,21 @@ class FlatParams:
 
         if self.half is None:
             self.half = torch.empty(self.numel, dtype=torch.bfloat16, device=self.device)
+        if self._checked and self.half_version >= 0:
+            return self.half
         v = self.version()
+        self._checked = True
         if v != self.half_version:
             ops.cast_bf16(self.data, self.half)
             self.half_version = v
             self.refresh_half_t()
         return self.half
+
+    def begin_pass(self) -> None:
+        """Start of the owning model's forward: the next bf16() compares the version signature
+        (O(#params) host work) once; every other weight fetch of the pass -- and of its
+        backward -- reuses that result instead of re-summing per GEMM launch."""
+        self._checked = False
 
     def version(self) -> int:
         # in-place updates through a Parameter bump that Parameter's own counter
@@ -114,6 +124,7 @@ class FlatParams:
         """Called by the fused optimizer right after it rewrote the bf16 copy (same stream):
         the transposed copies follow in the same stream order (and the same captured graph)."""
         self.half_version = self.version()
+        self._checked = True
         self.refresh_half_t()
 
     def half_view(self, p):

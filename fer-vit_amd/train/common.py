@@ -47,7 +47,7 @@ def clip_gradients(model, optimizer, max_norm: float) -> None:
     """clip_grad_norm_ without a host round trip: on the flat gradient buffer (coefficient
     consumed by FusedAdamW) or torch's for other optimizers."""
     if isinstance(optimizer, FusedAdamW) and hasattr(_core(model), "fer_flat"):
-        fused_clip_grad_norm_(_core(model), max_norm)
+        fused_clip_grad_norm_(_core(model), max_norm, optimizer=optimizer)
     else:
         torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm)
 
@@ -75,8 +75,8 @@ class EpochStats:
             "accuracy": accuracy_score(labels, preds),
             "f1_macro": f1_score(labels, preds, average="macro"),
             "f1_weighted": f1_score(labels, preds, average="weighted"),
-            "predictions": list(preds),
-            "labels": list(labels),
+            "predictions": preds.tolist(),
+            "labels": labels.tolist(),
         }
 
 

@@ -17,8 +17,14 @@
  *  - Every call enqueues on `stream` and never synchronises the host.
  *  - Return 0 on success, a negative code on error; fer_last_error() then
  *    returns a thread-local message. No C++ exception crosses the ABI.
- *  - Dropout masks are regenerated from (seed, element index); callers pass
- *    drop_thresh = (uint32)(p * 2^32) (0 = off) and drop_scale = 1/(1-p).
+ *  - Dropout masks are regenerated from (seed, element index): element i is
+ *    dropped iff its 16-bit uniform u16(i) < drop_thresh. Callers pass
+ *    drop_thresh = round(p * 65536) clamped to [1, 65535] for 0 < p < 1,
+ *    0 = dropout off (p = 0), 65536 = drop everything (p = 1, with drop_scale 0);
+ *    drop_scale = 1/(1-p). (fervit/ops.py drop_args is the reference encoder.)
+ *  - Gradient all-reduce (DDP) is NOT in this ABI: the Python host issues it through
+ *    torch.distributed's "nccl" backend (= RCCL on ROCm) on a side stream, ordered against
+ *    these kernels by HIP events (fervit/ddp.py). No fer_rccl_* entry points exist.
  */
 #ifndef FERVIT_H
 #define FERVIT_H

@@ -82,3 +82,39 @@ def test_graph_replays_draw_fresh_dropout_masks(p):
         assert losses[0] == losses[1] == losses[2]
     else:
         assert len(set(losses)) == 3
+
+
+def test_release_folds_replays_into_step_count():
+    """After StepGraph.release the optimizer's host step counts include the replays: a
+    checkpoint taken then, and eager steps after it, continue the bias correction exactly as
+    an all-eager run (graph-mode step count)."""
+    from fervit.graph import StepGraph
+    from fervit.optim import FusedAdamW
+
+    x, y = batch()
+    ma, crit = make(0.0)
+    oa = FusedAdamW(ma.parameters(), lr=1e-3, weight_decay=0.05, model=ma)
+    mb, _ = make(0.0)
+    ob = FusedAdamW(mb.parameters(), lr=1e-3, weight_decay=0.05, model=mb)
+
+    def step(m, o):
+        o.zero_grad(set_to_none=True)
+        loss = crit(m(x), y)
+        loss.backward()
+        o.step()
+        return loss
+
+    for _ in range(8):
+        step(ma, oa)
+    sg = StepGraph(lambda: step(mb, ob), ob, warmup=2).capture()
+    for _ in range(4):
+        sg.replay()
+    sg.release()
+    steps = {int(v["step"]) for v in ob.state_dict()["state"].values()}
+    assert steps == {6}, steps
+    for _ in range(2):
+        step(mb, ob)
+    torch.cuda.synchronize()
+    for pa, pb in zip(ma.parameters(), mb.parameters()):
+        assert (pa.detach() - pb.detach()).abs().max().item() <= 1e-6
+    assert {int(v["step"]) for v in ob.state_dict()["state"].values()} == {8}
