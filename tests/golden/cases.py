@@ -45,7 +45,16 @@ def fixture_state_dict(fx: Dict[str, np.ndarray]) -> Dict[str, torch.Tensor]:
 
 
 def case_inputs(name: str):
+    """The case's deterministic inputs; fixtures built under the margin rule (make_golden.py
+    pick_rows) name the rows they kept out of a 3x pool."""
     c = CASES[name]
+    fx = load_fixture(name)
+    if "input_rows" in fx:
+        B = c["input_shape"][0]
+        rows = torch.from_numpy(fx["input_rows"].astype(np.int64))
+        x = det_input(name, (3 * B,) + tuple(c["input_shape"][1:]))[rows]
+        y = det_labels(name, 3 * B)[rows]
+        return x, y
     x = det_input(name, c["input_shape"])
     y = det_labels(name, c["input_shape"][0])
     return x, y
@@ -65,3 +74,25 @@ def oracle_forward(name: str, x: torch.Tensor, p: Dict[str, torch.Tensor]) -> to
                                        a.get("use_lwn", False), a.get("use_lwn_residual", False),
                                        a.get("use_leam", False))
     raise ValueError(name)
+
+
+# ------------------------------------------------------------------ hybrid pieces (timm-free)
+ADAPTER_KEYS = [("alpha", (1,)), ("adapter.0.weight", (64, 768)), ("adapter.0.bias", (64,)),
+                ("adapter.2.weight", (768, 64)), ("adapter.2.bias", (768,))]
+
+
+def adapter_inputs():
+    """State dict, x [4,19,768] and dy of the `adapter` fixture (make_golden.adapter_case)."""
+    sd = det_state_dict(ADAPTER_KEYS)
+    sd["alpha"] = torch.tensor([0.37])
+    return sd, det_input("adapter_x", (4, 19, 768)), det_input("adapter_dy", (4, 19, 768))
+
+
+def check_summary(fx, key: str, t: torch.Tensor, rel: float) -> None:
+    """t against a {sum, L2, samples} record: L2 and every sample within rel * L2-scale."""
+    f = t.detach().reshape(-1).double().cpu()
+    l2 = float(fx[key + ":l2"])
+    assert abs(f.norm().item() - l2) <= rel * l2 + 1e-6, (key, f.norm().item(), l2)
+    scale = l2 / max(1.0, f.numel()) ** 0.5  # rms element
+    np.testing.assert_allclose(f[fx[key + ":idx"]].numpy(), fx[key + ":samples"], rtol=rel,
+                               atol=rel * max(scale, 1e-6) * 4, err_msg=key)

@@ -88,7 +88,78 @@ def run_case(name: str, model: torch.nn.Module, x: torch.Tensor, labels: torch.T
     print(f"{name}: loss={rec['loss']:.6f} logits[0]={rec['logits'][0][:3]} min-margin={rec['margin'].min():.3g}")
 
 
+def pick_rows(model: torch.nn.Module, name: str, shape, need: int, min_margin: float = 1e-2):
+    """SURVEY §7 fixture rule: keep only samples whose top-1 / top-2 logit margin is >= 1e-2, so
+    argmax equality is well posed. Draws a pool of 3x `need` deterministic inputs, runs the
+    reference forward (train mode, dropout 0: per-sample, no batch coupling) and returns the
+    first `need` rows that pass (their pool indices are stored in the fixture)."""
+    pool = det_input(name, (3 * need,) + tuple(shape[1:]))
+    load_det(model)
+    model.train()
+    with torch.no_grad():
+        lg = model(pool)
+    top = torch.topk(lg, 2, dim=1).values
+    ok = ((top[:, 0] - top[:, 1]) >= min_margin).nonzero().flatten()[:need]
+    assert ok.numel() == need, f"{name}: only {ok.numel()} samples pass the margin rule"
+    labels = det_labels(name, 3 * need)[ok]
+    return pool[ok], labels, ok.numpy()
+
+
+def adapter_case(out: dict) -> None:
+    """AdapterModule (`hybrid_latent_vit.py:249-265`) at the cfg4 geometry (768 -> 64 -> 768),
+    det weights, x [4,19,768]; forward, and backward of sum(y * dy) for det dy."""
+    from models_fer_vit.hybrid_latent_vit import AdapterModule
+
+    m = AdapterModule(768, 64)
+    load_det(m)
+    with torch.no_grad():
+        m.alpha.fill_(0.37)  # away from the init so the residual branch carries weight
+    x = det_input("adapter_x", (4, 19, 768)).requires_grad_(True)
+    dy = det_input("adapter_dy", (4, 19, 768))
+    y = m(x)
+    (y * dy).sum().backward()
+    rec = {"alpha": np.float32(0.37)}
+    tensors = {"y": y.detach(), "dx": x.grad}
+    tensors.update({"grad:" + k: p.grad for k, p in m.named_parameters()})
+    for k, t in tensors.items():
+        put_summary(rec, k, t)
+    out["adapter"] = rec
+    print("adapter: |y|", float(y.detach().norm()))
+
+
+def pos_interp_case(out: dict) -> None:
+    """HybridLatentViT._init_position_embedding (`hybrid_latent_vit.py:118-156`) on a det
+    ViT-B pos_embed [1,197,768]: seq_len 18 (w+), 36 (concat decomposer) and 196 (no interp).
+    The method only reads `pretrained_vit.pos_embed` (and self.embed_dim when there is none)."""
+    import types
+
+    from models_fer_vit.hybrid_latent_vit import HybridLatentViT
+
+    pe = torch.nn.Parameter(det_input("pos_embed_vitb", (1, 197, 768)))
+    stub = types.SimpleNamespace(pos_embed=pe)
+    me = types.SimpleNamespace(embed_dim=768)
+    rec = {}
+    for L in (18, 36, 196):
+        r = HybridLatentViT._init_position_embedding(me, stub, L).detach()
+        rec[f"L{L}:shape"] = np.array(r.shape)
+        if L < 196:
+            rec[f"L{L}"] = r[0, :, :64].numpy().copy()  # every position, first 64 channels
+        put_summary(rec, f"L{L}", r)
+    out["pos_interp"] = rec
+
+
+def put_summary(rec: dict, key: str, t: torch.Tensor, k: int = 256) -> None:
+    """Large tensors go in as {sum, L2, k fixed-index samples} (fixtures stay small)."""
+    f = t.detach().reshape(-1).double()
+    idx = sample_idx(key, f.numel(), k)
+    rec[key + ":sum"] = np.float64(f.sum().item())
+    rec[key + ":l2"] = np.float64(f.norm().item())
+    rec[key + ":idx"] = idx
+    rec[key + ":samples"] = f[idx].numpy()
+
+
 def main() -> None:
+    only = set(sys.argv[1:])
     sys.path.insert(0, REF)
     torch.set_num_threads(8)
     from models_fer_vit.image_vit import ImageViT
@@ -110,8 +181,9 @@ def main() -> None:
     run_case("latent_vit", m, det_input("latent_vit", (8, 18, 512)), det_labels("latent_vit", 8), cases)
     # LatentViTv2 with every prologue flag
     m = LatentViTv2(dropout=0.0, use_lwn=True, use_lwn_residual=True, use_spe=True, use_leam=True)
-    run_case("latent_vit_v2_all", m, det_input("latent_vit_v2_all", (8, 18, 512)),
-             det_labels("latent_vit_v2_all", 8), cases)
+    xs, ys, rows = pick_rows(m, "latent_vit_v2_all", (8, 18, 512), 8)
+    run_case("latent_vit_v2_all", m, xs, ys, cases)
+    cases["latent_vit_v2_all"]["input_rows"] = rows
     # LatentViTv2, LWN without residual gate, + LEAM, small depth/heads variant
     m = LatentViTv2(dropout=0.0, depth=2, heads=4, mlp_dim=1024, use_lwn=True, use_leam=True)
     run_case("latent_vit_v2_lwn", m, det_input("latent_vit_v2_lwn", (4, 18, 512)),
@@ -136,8 +208,12 @@ def main() -> None:
         with torch.no_grad():
             drec[f"{dm}:scores"] = dec.get_expression_scores(w).numpy()
     cases["decomposer"] = drec
+    adapter_case(cases)
+    pos_interp_case(cases)
 
     for name, rec in cases.items():
+        if only and name not in only:
+            continue
         np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **rec)
     print("wrote", len(cases), "fixtures")
 

@@ -75,3 +75,39 @@ def test_cross_entropy_class_weights_matches_torch():
     for ls in (0.0, 0.1):
         ref = torch.nn.functional.cross_entropy(logits, y, weight=w, label_smoothing=ls)
         assert abs(O.cross_entropy(logits, y, ls, w).item() - ref.item()) < 1e-6
+
+
+def test_oracle_adapter_matches_reference():
+    """AdapterModule (`hybrid_latent_vit.py:249-265`) restated in the oracle == the reference's
+    output and gradients on the committed fixture (cfg4 geometry 768 -> 64)."""
+    from cases import adapter_inputs, check_summary
+
+    fx = load_fixture("adapter")
+    sd, x, dy = adapter_inputs()
+    p = {k: v.clone().requires_grad_(True) for k, v in sd.items()}
+    x = x.clone().requires_grad_(True)
+    y = O.adapter(x, p, "")
+    (y * dy).sum().backward()
+    check_summary(fx, "y", y, 1e-5)
+    check_summary(fx, "dx", x.grad, 1e-5)
+    for k in sd:
+        check_summary(fx, "grad:" + k, p[k].grad, 1e-5)
+
+
+def test_pos_embed_interpolation_matches_reference():
+    """HybridLatentViT._init_position_embedding here == the reference's (`hybrid_latent_vit.py:
+    118-156`) for seq_len 18 (w+), 36 (concat) and 196 (kept): same torch calls, bit-exact."""
+    import types
+
+    from cases import check_summary
+    from models_fer_vit.hybrid_latent_vit import HybridLatentViT
+
+    fx = load_fixture("pos_interp")
+    pe = torch.nn.Parameter(det_input("pos_embed_vitb", (1, 197, 768)))
+    stub = types.SimpleNamespace(pos_embed=pe)
+    for L in (18, 36, 196):
+        r = HybridLatentViT._init_position_embedding(types.SimpleNamespace(embed_dim=768), stub, L).detach()
+        assert tuple(r.shape) == tuple(fx[f"L{L}:shape"])
+        if L < 196:
+            np.testing.assert_array_equal(r[0, :, :64].numpy(), fx[f"L{L}"])
+        check_summary(fx, f"L{L}", r, 1e-7)
