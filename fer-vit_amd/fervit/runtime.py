@@ -73,6 +73,7 @@ class FlatParams:
         self.half: Optional[torch.Tensor] = None
         self.half_version = -1
         self._checked = False  # version signature already compared during this forward pass
+        self._passes = False  # set by the owning module's forward (begin_pass): enables the cache
         self.half_t: Optional[torch.Tensor] = None  # transposed bf16 copies of the 2-D params
         self._tsegs: Optional[torch.Tensor] = None
         self._ttiles = 0
@@ -99,7 +100,7 @@ class FlatParams:
 
         if self.half is None:
             self.half = torch.empty(self.numel, dtype=torch.bfloat16, device=self.device)
-        if self._checked and self.half_version >= 0:
+        if self._passes and self._checked and self.half_version >= 0:
             return self.half
         v = self.version()
         self._checked = True
@@ -113,6 +114,7 @@ class FlatParams:
         """Start of the owning model's forward: the next bf16() compares the version signature
         (O(#params) host work) once; every other weight fetch of the pass -- and of its
         backward -- reuses that result instead of re-summing per GEMM launch."""
+        self._passes = True
         self._checked = False
 
     def version(self) -> int:

@@ -19,4 +19,4 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun
   || { tail -20 gpurun_out/prof_$TAG.log; exit 1; }
 tail -1 gpurun_out/prof_$TAG.log
 f=$(find gpurun_out/prof_$TAG -name '*kernel_stats.csv' | head -1)
-python tools/prof_csv_summary.py "$f" 13 30 > gpurun_out/prof_${TAG}_summary.txt && cat gpurun_out/prof_${TAG}_summary.txt
+python tools/prof_csv_summary.py "$f" 15 30 > gpurun_out/prof_${TAG}_summary.txt && cat gpurun_out/prof_${TAG}_summary.txt
