@@ -110,15 +110,16 @@ FER_DEV void img_dma(char* img, __amdgpu_buffer_rsrc_t rs, long row0, long ld, i
   }
 }
 
-FER_DEV void store_rows_q(bf16* o, const f32x16 (&acc)[2], float mul, int hh, int dh) {
+FER_DEV void store_rows_q(bf16* o, const f32x16& a0, const f32x16& a1, float mul, int hh, int dh) {
 #pragma unroll
   for (int db = 0; db < 2; ++db)
 #pragma unroll
     for (int g4 = 0; g4 < 4; ++g4) {
+      const f32x16& a = db ? a1 : a0;
       const int d = db * 32 + 8 * g4 + 4 * hh;
       if (d < dh)
-        *(bf16x4*)(o + d) = bf16x4{(bf16)(acc[db][4 * g4] * mul), (bf16)(acc[db][4 * g4 + 1] * mul),
-                                   (bf16)(acc[db][4 * g4 + 2] * mul), (bf16)(acc[db][4 * g4 + 3] * mul)};
+        *(bf16x4*)(o + d) = bf16x4{(bf16)(a[4 * g4] * mul), (bf16)(a[4 * g4 + 1] * mul),
+                                   (bf16)(a[4 * g4 + 2] * mul), (bf16)(a[4 * g4 + 3] * mul)};
     }
 }
 
@@ -187,206 +188,8 @@ __global__ __launch_bounds__(64 * NB) __attribute__((amdgpu_waves_per_eu(4))) vo
   }
   l += __shfl_xor(l, 32, 64);
   if (q < N) {
-    store_rows_q(out + ((long)b * N + q) * ldo + h * dh, ot, 1.f / l, hh, dh);
+    store_rows_q(out + ((long)b * N + q) * ldo + h * dh, ot[0], ot[1], 1.f / l, hh, dh);
     if (hh == 0) lse[(long)bh * N + q] = (m + log2f(l)) * LN2;
-  }
-}
-
-// ---------------------------------------------------------------- backward, dQ
-// Wave w = query block w; K, V images by LDS-DMA. Per key block: S^T, dP^T = V dO^T,
-// dS^T = P^T o (dropout'(dP^T) - Dq), dQ^T += K^T dS^T.   Dq = rowsum(dO o O) per query.
-template <int NB>
-__global__ __launch_bounds__(64 * NB) __attribute__((amdgpu_waves_per_eu(4))) void attn_dq_bf16(const bf16* __restrict__ qkv, long ldq,
-                                                         const bf16* __restrict__ out, long ldo,
-                                                         const bf16* __restrict__ dout, long lddo,
-                                                         const float* __restrict__ lse, bf16* __restrict__ dqkv,
-                                                         long lddq, int N, int H, int dh, float scale, float sl2,
-                                                         uint32_t thr, float dscale, uint64_t seed) {
-  seed = step_seed(seed);
-  __shared__ __attribute__((aligned(1024))) char lds[2 * NB * 32 * 128];
-  char* Ki = lds;
-  char* Vi = lds + NB * 32 * 128;
-  const int bh = blockIdx.x, b = bh / H, h = bh - b * H, D = H * dh;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hh = lane >> 5;
-  const __amdgpu_buffer_rsrc_t rs = make_rsrc(qkv);
-  img_dma<NB>(Ki, rs, (long)b * N, ldq, D + h * dh, N, dh, w, lane);
-  img_dma<NB>(Vi, rs, (long)b * N, ldq, 2 * D + h * dh, N, dh, w, lane);
-
-  const int q = w * 32 + (lane & 31);
-  const bool qv = q < N;
-  bf16x8 qf[4], of[4];
-  float dsum = 0.f;
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    const int d0 = 16 * s + 8 * hh;
-    const bool ok = qv && d0 < dh;
-    qf[s] = ok ? *(const bf16x8*)(qkv + ((long)b * N + q) * ldq + h * dh + d0) : bf16x8{};
-    of[s] = ok ? *(const bf16x8*)(dout + ((long)b * N + q) * lddo + h * dh + d0) : bf16x8{};
-    const bf16x8 ov = ok ? *(const bf16x8*)(out + ((long)b * N + q) * ldo + h * dh + d0) : bf16x8{};
-#pragma unroll
-    for (int j = 0; j < 8; ++j) dsum += (float)ov[j] * (float)of[s][j];
-  }
-  dsum += __shfl_xor(dsum, 32, 64);
-  const float lq = qv ? lse[(long)bh * N + q] * LOG2E : INFINITY;
-  __syncthreads();
-
-  const uint32_t row = drop_row(bh, N, q);
-  f32x16 dqt[2] = {f32x16{}, f32x16{}};
-#pragma unroll 1
-  for (int kb = 0; kb < NB; ++kb) {
-    f32x16 st = {}, dp = {};
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      st = mfma32(rd_row(Ki, kb * 32 + (lane & 31), 2 * s + hh), qf[s], st);
-      dp = mfma32(rd_row(Vi, kb * 32 + (lane & 31), 2 * s + hh), of[s], dp);
-    }
-    if (thr) drop16_keys(seed, row, kb, hh, thr, dscale, dp);
-    const bool tail = kb * 32 + 32 > N;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      float p = ex2(fmaf(st[r], sl2, -lq));
-      if (tail && kb * 32 + acc_row(r, hh) >= N) p = 0.f;
-      st[r] = p * (dp[r] - dsum);
-    }
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      const bf16x8 df = pack8(st, s2);
-#pragma unroll
-      for (int db = 0; db < 2; ++db) dqt[db] = mfma32(rd_tr(Ki, kb * 32 + 16 * s2, db * 32, lane), df, dqt[db]);
-    }
-  }
-  if (qv) store_rows_q(dqkv + ((long)b * N + q) * lddq + h * dh, dqt, scale, hh, dh);
-}
-
-// ---------------------------------------------------------------- backward, dK dV
-// Wave w = key block w; Q and dO images by LDS-DMA, lse and Dq in LDS. Per query block:
-// S = Q K^T, dP = dO V^T (registers hold queries), dV += P_drop^T dO, dK += dS^T Q.
-// The dropout hash pairs are consecutive KEYS = neighbouring lanes here: each lane of a pair
-// hashes 8 of the 16 query rows and swaps them with its neighbour.
-template <int NB>
-__global__ __launch_bounds__(64 * NB) void attn_dkv_bf16(const bf16* __restrict__ qkv, long ldq,
-                                                          const bf16* __restrict__ out, long ldo,
-                                                          const bf16* __restrict__ dout, long lddo,
-                                                          const float* __restrict__ lse, bf16* __restrict__ dqkv,
-                                                          long lddq, int N, int H, int dh, float scale, float sl2,
-                                                          uint32_t thr, float dscale, uint64_t seed) {
-  seed = step_seed(seed);
-  constexpr int IMG = NB * 32 * 128;
-  __shared__ __attribute__((aligned(1024))) char lds[2 * IMG + 2 * NB * 32 * 4];
-  char* Qi = lds;
-  char* Oi = lds + IMG;  // dO image
-  float* lse_s = (float*)(lds + 2 * IMG);
-  float* dd_s = lse_s + NB * 32;
-  const int bh = blockIdx.x, b = bh / H, h = bh - b * H, D = H * dh;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hh = lane >> 5;
-  img_dma<NB>(Qi, make_rsrc(qkv), (long)b * N, ldq, h * dh, N, dh, w, lane);
-  img_dma<NB>(Oi, make_rsrc(dout), (long)b * N, lddo, h * dh, N, dh, w, lane);
-
-  // Dq = rowsum(dO o O): two threads per query row
-  for (int t = threadIdx.x; t < NB * 64; t += 64 * NB) {
-    const int qr = t >> 1, half = t & 1;
-    float dsum = 0.f;
-    if (qr < N) {
-      const bf16* po = out + ((long)b * N + qr) * ldo + h * dh;
-      const bf16* pd = dout + ((long)b * N + qr) * lddo + h * dh;
-      for (int d = half * 8; d < dh; d += 16) {
-        const bf16x8 a = *(const bf16x8*)(po + d), c = *(const bf16x8*)(pd + d);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) dsum += (float)a[j] * (float)c[j];
-      }
-    }
-    dsum += __shfl_xor(dsum, 1, 64);
-    if (!half) {
-      dd_s[qr] = dsum;
-      lse_s[qr] = qr < N ? lse[(long)bh * N + qr] * LOG2E : INFINITY;
-    }
-  }
-  const int key = w * 32 + (lane & 31);
-  const bool kval = key < N;
-  bf16x8 kf[4], vf[4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    const int d0 = 16 * s + 8 * hh;
-    const bool ok = kval && d0 < dh;
-    kf[s] = ok ? *(const bf16x8*)(qkv + ((long)b * N + key) * ldq + D + h * dh + d0) : bf16x8{};
-    vf[s] = ok ? *(const bf16x8*)(qkv + ((long)b * N + key) * ldq + 2 * D + h * dh + d0) : bf16x8{};
-  }
-  __syncthreads();
-
-  const int NP = N + (N & 1);
-  const bool odd = lane & 1;
-  f32x16 dk[2] = {f32x16{}, f32x16{}}, dv[2] = {f32x16{}, f32x16{}};
-#pragma unroll
-  for (int qb = 0; qb < NB; ++qb) {
-    f32x16 st = {}, dp = {};
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      st = mfma32(rd_row(Qi, qb * 32 + (lane & 31), 2 * s + hh), kf[s], st);
-      dp = mfma32(rd_row(Oi, qb * 32 + (lane & 31), 2 * s + hh), vf[s], dp);
-    }
-    uint32_t keep = 0xFFFFu;
-    if (thr) {
-      // this lane hashes rows [8*odd, 8*odd + 8) for the key pair (key & ~1, key | 1)
-      uint32_t hv[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int r = 8 * odd + i;
-        const int qr = qb * 32 + acc_row(r, hh);
-        hv[i] = fer_hash(seed, (((uint32_t)bh * N + qr) * (uint32_t)NP + (uint32_t)(key & ~1)) >> 1);
-      }
-      keep = 0;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const uint32_t other = (uint32_t)__shfl_xor((int)hv[i], 1, 64);
-        const uint32_t h_lo = odd ? other : hv[i];  // rows i (even lane's own)
-        const uint32_t h_hi = odd ? hv[i] : other;  // rows 8 + i
-        const uint32_t u_lo = odd ? (h_lo >> 16) : (h_lo & 0xFFFFu);
-        const uint32_t u_hi = odd ? (h_hi >> 16) : (h_hi & 0xFFFFu);
-        keep |= (uint32_t)(u_lo >= thr) << i;
-        keep |= (uint32_t)(u_hi >= thr) << (8 + i);
-      }
-    }
-    f32x16 pd;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int qr = qb * 32 + acc_row(r, hh);
-      const float p = kval ? ex2(fmaf(st[r], sl2, -lse_s[qr])) : 0.f;
-      const bool kp = (keep >> r) & 1;
-      const float g = thr ? (kp ? dp[r] * dscale : 0.f) : dp[r];
-      pd[r] = thr ? (kp ? p * dscale : 0.f) : p;
-      st[r] = p * (g - dd_s[qr]);
-    }
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      const bf16x8 pf = pack8(pd, s2), df = pack8(st, s2);
-#pragma unroll
-      for (int db = 0; db < 2; ++db) {
-        dv[db] = mfma32(pf, rd_tr(Oi, qb * 32 + 16 * s2, db * 32, lane), dv[db]);
-        dk[db] = mfma32(df, rd_tr(Qi, qb * 32 + 16 * s2, db * 32, lane), dk[db]);
-      }
-    }
-  }
-  // dk/dv[db][r]: key row = w*32 + acc_row(r, hh), d = db*32 + (lane&31). Stage each wave's
-  // 32 x 64 tiles through LDS (rows of 128 B, no reuse across waves) for 16-byte row stores.
-  __syncthreads();
-  bf16* stg = (bf16*)(lds + w * 8192);  // [2][32][64]
-#pragma unroll
-  for (int db = 0; db < 2; ++db)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int kr = acc_row(r, hh), d = db * 32 + (lane & 31);
-      stg[kr * 64 + d] = (bf16)(dk[db][r] * scale);
-      stg[2048 + kr * 64 + d] = (bf16)dv[db][r];
-    }
-  // (wave-private region: LDS accesses of one wave complete in order)
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int t = i * 64 + lane;          // 512 chunks of 16 B: [2 mats][32 rows][8 chunks]
-    const int mat = t >> 8, kr = (t >> 3) & 31, c = t & 7;
-    const int gk = w * 32 + kr;
-    if (gk < N && c * 8 < dh)
-      *(bf16x8*)(dqkv + ((long)b * N + gk) * lddq + (1 + mat) * D + h * dh + c * 8) =
-          *(const bf16x8*)(stg + mat * 2048 + kr * 64 + c * 8);
   }
 }
 
@@ -647,6 +450,329 @@ __global__ __launch_bounds__(64 * NB) void attn_bwd_fused_bf16(const bf16* __res
   }
 }
 
+// ---------------------------------------------------------------- general path
+// Any N, dh <= 128 (dh % 8 == 0): the head dimension in DH2 halves of 64 columns (each half is
+// one swizzled [rows][128 B] image, so every address helper above is reused unchanged), keys /
+// queries streamed through LDS in chunks of 128 rows. Workgroup = 4 waves = 128 queries (forward,
+// dQ) or 128 keys (dK/dV) of one (batch, head); grid.y walks the chunks of the sequence. Used
+// where the single-workgroup-per-head kernels do not fit (N > 256 or dh > 64): e.g. LatentViTv2
+// with heads=4 (dh = 128, `latent_vit.py:24-31` accepts any head count).
+constexpr int GEN_ROWS = 128;
+constexpr int GEN_IMG = GEN_ROWS * 128;  // one 64-column half of a 128-row chunk
+
+// chunk rows [row0, row0 + 128) of the column block col0 (DH2 halves) -> DH2 images
+template <int DH2>
+FER_DEV void gen_dma(char* img, __amdgpu_buffer_rsrc_t rs, long row0, long ld, int col0, int nrows, int dh, int w,
+                     int lane) {
+#pragma unroll
+  for (int hf = 0; hf < DH2; ++hf)
+    img_dma<4>(img + hf * GEN_IMG, rs, row0, ld, col0 + 64 * hf, nrows, dh - 64 * hf, w, lane);
+}
+
+template <int DH2>
+__global__ __launch_bounds__(256) void attn_fwd_gen(const bf16* __restrict__ qkv, long ldq, bf16* __restrict__ out,
+                                                    long ldo, float* __restrict__ lse, int N, int H, int dh,
+                                                    float sl2, uint32_t thr, float dscale, uint64_t seed) {
+  seed = step_seed(seed);
+  __shared__ __attribute__((aligned(1024))) char lds[2 * DH2 * GEN_IMG];
+  char* Ki = lds;
+  char* Vi = lds + DH2 * GEN_IMG;
+  const int bh = blockIdx.x, b = bh / H, h = bh - b * H, D = H * dh;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hh = lane >> 5;
+  const int q = blockIdx.y * GEN_ROWS + w * 32 + (lane & 31);
+  const bool qv = q < N;
+  const __amdgpu_buffer_rsrc_t rs = make_rsrc(qkv);
+  bf16x8 qf[4 * DH2];
+#pragma unroll
+  for (int s = 0; s < 4 * DH2; ++s) {
+    const int d0 = 16 * s + 8 * hh;
+    qf[s] = (qv && d0 < dh) ? *(const bf16x8*)(qkv + ((long)b * N + q) * ldq + h * dh + d0) : bf16x8{};
+  }
+  const uint32_t row = drop_row(bh, N, q);
+  float m = -INFINITY, l = 0.f;
+  f32x16 ot[2 * DH2];
+#pragma unroll
+  for (int j = 0; j < 2 * DH2; ++j) ot[j] = f32x16{};
+#pragma unroll 1
+  for (int c0 = 0; c0 < N; c0 += GEN_ROWS) {
+    if (c0) __syncthreads();  // every wave is done with the previous chunk's images
+    gen_dma<DH2>(Ki, rs, (long)b * N + c0, ldq, D + h * dh, N - c0, dh, w, lane);
+    gen_dma<DH2>(Vi, rs, (long)b * N + c0, ldq, 2 * D + h * dh, N - c0, dh, w, lane);
+    wait_vm<0>();
+    __syncthreads();
+    const int nkb = min(GEN_ROWS / 32, (N - c0 + 31) / 32);
+#pragma unroll 1
+    for (int kb = 0; kb < nkb; ++kb) {
+      const int kg = c0 / 32 + kb;  // global key block
+      f32x16 st = {};
+#pragma unroll
+      for (int hf = 0; hf < DH2; ++hf)
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+          st = mfma32(rd_row(Ki + hf * GEN_IMG, kb * 32 + (lane & 31), 2 * s + hh), qf[4 * hf + s], st);
+      if (kg * 32 + 32 > N) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (kg * 32 + acc_row(r, hh) >= N) st[r] = -INFINITY;
+      }
+      float bm = st[0];
+#pragma unroll
+      for (int r = 1; r < 16; ++r) bm = fmaxf(bm, st[r]);
+      bm = fmaxf(bm, __shfl_xor(bm, 32, 64)) * sl2;
+      const float mn = fmaxf(m, bm);
+      const float al = ex2(m - mn);
+      m = mn;
+      l *= al;
+#pragma unroll
+      for (int j = 0; j < 2 * DH2; ++j) ot[j] *= al;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        st[r] = ex2(fmaf(st[r], sl2, -mn));
+        l += st[r];
+      }
+      if (thr) drop16_keys(seed, row, kg, hh, thr, dscale, st);
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const bf16x8 pf = pack8(st, s2);
+#pragma unroll
+        for (int hf = 0; hf < DH2; ++hf)
+#pragma unroll
+          for (int db = 0; db < 2; ++db)
+            ot[2 * hf + db] = mfma32(rd_tr(Vi + hf * GEN_IMG, kb * 32 + 16 * s2, db * 32, lane), pf, ot[2 * hf + db]);
+      }
+    }
+  }
+  l += __shfl_xor(l, 32, 64);
+  if (qv) {
+#pragma unroll
+    for (int hf = 0; hf < DH2; ++hf)
+      store_rows_q(out + ((long)b * N + q) * ldo + h * dh + 64 * hf, ot[2 * hf], ot[2 * hf + 1], 1.f / l, hh,
+                   dh - 64 * hf);
+    if (hh == 0) lse[(long)bh * N + q] = (m + log2f(l)) * LN2;
+  }
+}
+
+// dQ: wave = query block; K, V streamed. Per key block: S^T, dP^T = V dO^T,
+// dS^T = P^T o (dropout'(dP^T) - Dq), dQ^T += K^T dS^T.   Dq = rowsum(dO o O).
+template <int DH2>
+__global__ __launch_bounds__(256) void attn_dq_gen(const bf16* __restrict__ qkv, long ldq,
+                                                   const bf16* __restrict__ out, long ldo,
+                                                   const bf16* __restrict__ dout, long lddo,
+                                                   const float* __restrict__ lse, bf16* __restrict__ dqkv, long lddq,
+                                                   int N, int H, int dh, float scale, float sl2, uint32_t thr,
+                                                   float dscale, uint64_t seed) {
+  seed = step_seed(seed);
+  __shared__ __attribute__((aligned(1024))) char lds[2 * DH2 * GEN_IMG];
+  char* Ki = lds;
+  char* Vi = lds + DH2 * GEN_IMG;
+  const int bh = blockIdx.x, b = bh / H, h = bh - b * H, D = H * dh;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hh = lane >> 5;
+  const int q = blockIdx.y * GEN_ROWS + w * 32 + (lane & 31);
+  const bool qv = q < N;
+  const __amdgpu_buffer_rsrc_t rs = make_rsrc(qkv);
+  bf16x8 qf[4 * DH2], of[4 * DH2];
+  float dsum = 0.f;
+#pragma unroll
+  for (int s = 0; s < 4 * DH2; ++s) {
+    const int d0 = 16 * s + 8 * hh;
+    const bool ok = qv && d0 < dh;
+    qf[s] = ok ? *(const bf16x8*)(qkv + ((long)b * N + q) * ldq + h * dh + d0) : bf16x8{};
+    of[s] = ok ? *(const bf16x8*)(dout + ((long)b * N + q) * lddo + h * dh + d0) : bf16x8{};
+    const bf16x8 ov = ok ? *(const bf16x8*)(out + ((long)b * N + q) * ldo + h * dh + d0) : bf16x8{};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dsum += (float)ov[j] * (float)of[s][j];
+  }
+  dsum += __shfl_xor(dsum, 32, 64);
+  const float lq = qv ? lse[(long)bh * N + q] * LOG2E : INFINITY;
+  const uint32_t row = drop_row(bh, N, q);
+  f32x16 dqt[2 * DH2];
+#pragma unroll
+  for (int j = 0; j < 2 * DH2; ++j) dqt[j] = f32x16{};
+#pragma unroll 1
+  for (int c0 = 0; c0 < N; c0 += GEN_ROWS) {
+    if (c0) __syncthreads();
+    gen_dma<DH2>(Ki, rs, (long)b * N + c0, ldq, D + h * dh, N - c0, dh, w, lane);
+    gen_dma<DH2>(Vi, rs, (long)b * N + c0, ldq, 2 * D + h * dh, N - c0, dh, w, lane);
+    wait_vm<0>();
+    __syncthreads();
+    const int nkb = min(GEN_ROWS / 32, (N - c0 + 31) / 32);
+#pragma unroll 1
+    for (int kb = 0; kb < nkb; ++kb) {
+      const int kg = c0 / 32 + kb;
+      f32x16 st = {}, dp = {};
+#pragma unroll
+      for (int hf = 0; hf < DH2; ++hf)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          st = mfma32(rd_row(Ki + hf * GEN_IMG, kb * 32 + (lane & 31), 2 * s + hh), qf[4 * hf + s], st);
+          dp = mfma32(rd_row(Vi + hf * GEN_IMG, kb * 32 + (lane & 31), 2 * s + hh), of[4 * hf + s], dp);
+        }
+      if (thr) drop16_keys(seed, row, kg, hh, thr, dscale, dp);
+      const bool tail = kg * 32 + 32 > N;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float p = ex2(fmaf(st[r], sl2, -lq));
+        if (tail && kg * 32 + acc_row(r, hh) >= N) p = 0.f;
+        st[r] = p * (dp[r] - dsum);
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const bf16x8 df = pack8(st, s2);
+#pragma unroll
+        for (int hf = 0; hf < DH2; ++hf)
+#pragma unroll
+          for (int db = 0; db < 2; ++db)
+            dqt[2 * hf + db] = mfma32(rd_tr(Ki + hf * GEN_IMG, kb * 32 + 16 * s2, db * 32, lane), df, dqt[2 * hf + db]);
+      }
+    }
+  }
+  if (qv) {
+#pragma unroll
+    for (int hf = 0; hf < DH2; ++hf)
+      store_rows_q(dqkv + ((long)b * N + q) * lddq + h * dh + 64 * hf, dqt[2 * hf], dqt[2 * hf + 1], scale, hh,
+                   dh - 64 * hf);
+  }
+}
+
+// dK, dV: wave = key block; Q and dO streamed (with lse and Dq of the chunk's queries in LDS).
+// S = Q K^T, dP = dO V^T (registers hold queries), dV += P_drop^T dO, dK += dS^T Q. The dropout
+// hash pairs are consecutive KEYS = neighbouring lanes: each lane of a pair hashes 8 of the 16
+// query rows and swaps them with its neighbour.
+template <int DH2>
+__global__ __launch_bounds__(256) void attn_dkv_gen(const bf16* __restrict__ qkv, long ldq,
+                                                    const bf16* __restrict__ out, long ldo,
+                                                    const bf16* __restrict__ dout, long lddo,
+                                                    const float* __restrict__ lse, bf16* __restrict__ dqkv, long lddq,
+                                                    int N, int H, int dh, float scale, float sl2, uint32_t thr,
+                                                    float dscale, uint64_t seed) {
+  seed = step_seed(seed);
+  __shared__ __attribute__((aligned(1024))) char lds[2 * DH2 * GEN_IMG + 2 * GEN_ROWS * 4];
+  char* Qi = lds;
+  char* Oi = lds + DH2 * GEN_IMG;  // dO images
+  float* lse_s = (float*)(lds + 2 * DH2 * GEN_IMG);
+  float* dd_s = lse_s + GEN_ROWS;
+  const int bh = blockIdx.x, b = bh / H, h = bh - b * H, D = H * dh;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hh = lane >> 5;
+  const int key = blockIdx.y * GEN_ROWS + w * 32 + (lane & 31);
+  const bool kval = key < N;
+  bf16x8 kf[4 * DH2], vf[4 * DH2];
+#pragma unroll
+  for (int s = 0; s < 4 * DH2; ++s) {
+    const int d0 = 16 * s + 8 * hh;
+    const bool ok = kval && d0 < dh;
+    kf[s] = ok ? *(const bf16x8*)(qkv + ((long)b * N + key) * ldq + D + h * dh + d0) : bf16x8{};
+    vf[s] = ok ? *(const bf16x8*)(qkv + ((long)b * N + key) * ldq + 2 * D + h * dh + d0) : bf16x8{};
+  }
+  const int NP = N + (N & 1);
+  const bool odd = lane & 1;
+  f32x16 dk[2 * DH2], dv[2 * DH2];
+#pragma unroll
+  for (int j = 0; j < 2 * DH2; ++j) dk[j] = dv[j] = f32x16{};
+#pragma unroll 1
+  for (int c0 = 0; c0 < N; c0 += GEN_ROWS) {
+    if (c0) __syncthreads();
+    gen_dma<DH2>(Qi, make_rsrc(qkv), (long)b * N + c0, ldq, h * dh, N - c0, dh, w, lane);
+    gen_dma<DH2>(Oi, make_rsrc(dout), (long)b * N + c0, lddo, h * dh, N - c0, dh, w, lane);
+    {  // lse and Dq = rowsum(dO o O) of the chunk's queries: two threads per row
+      const int qr = threadIdx.x >> 1, half = threadIdx.x & 1, qg = c0 + qr;
+      float dsum = 0.f;
+      if (qg < N) {
+        const bf16* po = out + ((long)b * N + qg) * ldo + h * dh;
+        const bf16* pd = dout + ((long)b * N + qg) * lddo + h * dh;
+        for (int d = half * 8; d < dh; d += 16) {
+          const bf16x8 a = *(const bf16x8*)(po + d), c = *(const bf16x8*)(pd + d);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) dsum += (float)a[j] * (float)c[j];
+        }
+      }
+      dsum += __shfl_xor(dsum, 1, 64);
+      if (!half) {
+        dd_s[qr] = dsum;
+        lse_s[qr] = qg < N ? lse[(long)bh * N + qg] * LOG2E : INFINITY;
+      }
+    }
+    wait_vm<0>();
+    __syncthreads();
+    const int nqb = min(GEN_ROWS / 32, (N - c0 + 31) / 32);
+#pragma unroll 1
+    for (int qb = 0; qb < nqb; ++qb) {
+      f32x16 st = {}, dp = {};
+#pragma unroll
+      for (int hf = 0; hf < DH2; ++hf)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          st = mfma32(rd_row(Qi + hf * GEN_IMG, qb * 32 + (lane & 31), 2 * s + hh), kf[4 * hf + s], st);
+          dp = mfma32(rd_row(Oi + hf * GEN_IMG, qb * 32 + (lane & 31), 2 * s + hh), vf[4 * hf + s], dp);
+        }
+      uint32_t keep = 0xFFFFu;
+      if (thr) {
+        uint32_t hv[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int qg = c0 + qb * 32 + acc_row(8 * odd + i, hh);
+          hv[i] = fer_hash(seed, (((uint32_t)bh * N + qg) * (uint32_t)NP + (uint32_t)(key & ~1)) >> 1);
+        }
+        keep = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const uint32_t other = (uint32_t)__shfl_xor((int)hv[i], 1, 64);
+          const uint32_t h_lo = odd ? other : hv[i];
+          const uint32_t h_hi = odd ? hv[i] : other;
+          const uint32_t u_lo = odd ? (h_lo >> 16) : (h_lo & 0xFFFFu);
+          const uint32_t u_hi = odd ? (h_hi >> 16) : (h_hi & 0xFFFFu);
+          keep |= (uint32_t)(u_lo >= thr) << i;
+          keep |= (uint32_t)(u_hi >= thr) << (8 + i);
+        }
+      }
+      f32x16 pd;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int qr = qb * 32 + acc_row(r, hh);
+        const float p = kval ? ex2(fmaf(st[r], sl2, -lse_s[qr])) : 0.f;
+        const bool kp = (keep >> r) & 1;
+        const float g = thr ? (kp ? dp[r] * dscale : 0.f) : dp[r];
+        pd[r] = thr ? (kp ? p * dscale : 0.f) : p;
+        st[r] = p * (g - dd_s[qr]);
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const bf16x8 pf = pack8(pd, s2), df = pack8(st, s2);
+#pragma unroll
+        for (int hf = 0; hf < DH2; ++hf)
+#pragma unroll
+          for (int db = 0; db < 2; ++db) {
+            dv[2 * hf + db] = mfma32(pf, rd_tr(Oi + hf * GEN_IMG, qb * 32 + 16 * s2, db * 32, lane), dv[2 * hf + db]);
+            dk[2 * hf + db] = mfma32(df, rd_tr(Qi + hf * GEN_IMG, qb * 32 + 16 * s2, db * 32, lane), dk[2 * hf + db]);
+          }
+      }
+    }
+  }
+  // dk/dv[2*hf+db][r]: key row = w*32 + acc_row(r, hh), d = 64*hf + db*32 + (lane&31). Stage each
+  // wave's [2 mats][32 rows][64*DH2] tile through LDS (wave-private region, inside the images) for
+  // 16-byte row stores.
+  __syncthreads();
+  constexpr int W = 64 * DH2;
+  bf16* stg = (bf16*)(lds + w * (2 * 32 * W * 2));
+#pragma unroll
+  for (int j = 0; j < 2 * DH2; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int kr = acc_row(r, hh), d = j * 32 + (lane & 31);
+      stg[kr * W + d] = (bf16)(dk[j][r] * scale);
+      stg[32 * W + kr * W + d] = (bf16)dv[j][r];
+    }
+#pragma unroll
+  for (int i = 0; i < 8 * DH2; ++i) {
+    const int t = i * 64 + lane;  // [2 mats][32 rows][W/8 chunks]
+    constexpr int CPR = W / 8;
+    const int mat = t / (32 * CPR), kr = (t / CPR) & 31, c = t % CPR;
+    const int gk = blockIdx.y * GEN_ROWS + w * 32 + kr;
+    if (gk < N && c * 8 < dh)
+      *(bf16x8*)(dqkv + ((long)b * N + gk) * lddq + (1 + mat) * D + h * dh + c * 8) =
+          *(const bf16x8*)(stg + mat * 32 * W + kr * W + c * 8);
+  }
+}
+
 // ------------------------------------------------------------------ fp32 path
 // ws layout: P [BH][N][N] (softmax probs, undropped), then G [BH][N][N]
 __global__ void attn_f32_scores(const float* qkv, long ldq, float* P, int B, int N, int H, int dh, float scale) {
@@ -753,7 +879,7 @@ int fer::set_step_ptr_attention(const uint64_t* p) { return set_step_ptr_here(p)
 extern "C" int64_t fer_attention_ws(int dtype, int B, int N, int H) {
   // fp32 path: P and dS slabs, then the stand-alone colsum pass's partials; bf16: the fused
   // bias-gradient partials [B][3*H*64]
-  const int64_t cs = std::max<int64_t>(fer_colsum_ws(B * N, 3 * H * 64), (int64_t)B * 3 * H * 64 * 4);
+  const int64_t cs = std::max<int64_t>(fer_colsum_ws(B * N, 3 * H * 128), (int64_t)B * 3 * H * 64 * 4);
   return (dtype == FER_F32 ? (int64_t)2 * B * H * N * N * 4 : 0) + cs;
 }
 
@@ -772,16 +898,26 @@ extern "C" int fer_attention_fwd(int dtype, const void* qkv, int64_t ld_qkv, voi
                        (long)ld_qkv, (float*)out, (long)ld_out, B, N, H, dh, drop_thresh, drop_scale, seed);
     return hip_check("attention_fwd_f32");
   }
-  if (N > 256 || dh > 64 || dh % 8) return set_error("attention_fwd(bf16): needs N <= 256, dh <= 64, dh % 8 == 0");
+  if (dh > 128 || dh % 8) return set_error("attention_fwd(bf16): needs dh <= 128, dh % 8 == 0");
   if (check_drop_range(drop_thresh, (long)B * H * N * (N + (N & 1)), "attention_fwd: dropout over >= 2^32 probabilities"))
     return -1;
   if (ld_qkv % 8 || ld_out % 4) return set_error("attention_fwd(bf16): misaligned leading dimension");
   if ((long)B * N * ld_qkv * 2 >= 0x7FFFFFF0L) return set_error("attention_fwd(bf16): qkv exceeds 2 GiB");
-  const int nb = (N + 31) / 32;
   const float sl2 = scale * LOG2E;
-  FER_NB_SWITCH(nb, hipLaunchKernelGGL(attn_fwd_bf16<NB_>, dim3(B * H), dim3(64 * NB_), 0, st, (const bf16*)qkv,
-                                       (long)ld_qkv, (bf16*)out, (long)ld_out, lse, N, H, dh, sl2, drop_thresh,
-                                       drop_scale, seed));
+  if (N <= 256 && dh <= 64) {
+    const int nb = (N + 31) / 32;
+    FER_NB_SWITCH(nb, hipLaunchKernelGGL(attn_fwd_bf16<NB_>, dim3(B * H), dim3(64 * NB_), 0, st, (const bf16*)qkv,
+                                         (long)ld_qkv, (bf16*)out, (long)ld_out, lse, N, H, dh, sl2, drop_thresh,
+                                         drop_scale, seed));
+  } else {
+    const dim3 grid(B * H, (N + GEN_ROWS - 1) / GEN_ROWS);
+    if (dh <= 64)
+      hipLaunchKernelGGL(attn_fwd_gen<1>, grid, dim3(256), 0, st, (const bf16*)qkv, (long)ld_qkv, (bf16*)out,
+                         (long)ld_out, lse, N, H, dh, sl2, drop_thresh, drop_scale, seed);
+    else
+      hipLaunchKernelGGL(attn_fwd_gen<2>, grid, dim3(256), 0, st, (const bf16*)qkv, (long)ld_qkv, (bf16*)out,
+                         (long)ld_out, lse, N, H, dh, sl2, drop_thresh, drop_scale, seed);
+  }
   return hip_check("attention_fwd_bf16");
 }
 
@@ -817,7 +953,7 @@ extern "C" int fer_attention_bwd(int dtype, const void* qkv, int64_t ld_qkv, con
     if (rc || !colsum) return rc;
     return colsum_pass(ws + 2 * pe, ws_bytes - 2 * pe * 4);
   }
-  if (N > 256 || dh > 64 || dh % 8) return set_error("attention_bwd(bf16): needs N <= 256, dh <= 64, dh % 8 == 0");
+  if (dh > 128 || dh % 8) return set_error("attention_bwd(bf16): needs dh <= 128, dh % 8 == 0");
   if (check_drop_range(drop_thresh, (long)B * H * N * (N + (N & 1)), "attention_bwd: dropout over >= 2^32 probabilities"))
     return -1;
   if (ld_qkv % 8 || ld_out % 8 || ld_dout % 8 || ld_dqkv % 8) return set_error("attention_bwd(bf16): misaligned ld");
@@ -825,9 +961,9 @@ extern "C" int fer_attention_bwd(int dtype, const void* qkv, int64_t ld_qkv, con
     return set_error("attention_bwd(bf16): operand exceeds 2 GiB (buffer-resource range)");
   const int nb = (N + 31) / 32;
   const float sl2 = scale * LOG2E;
-  static const bool two_kernel = getenv("FERVIT_ATTN_BWD_2K") != nullptr;  // A/B switch
+  static const bool general = getenv("FERVIT_ATTN_GENERAL") != nullptr;  // A/B switch: general path only
   static const int dbg = getenv("FERVIT_ATTN_DBG") ? atoi(getenv("FERVIT_ATTN_DBG")) : 0;  // timing experiments
-  if (nb <= 8 && !two_kernel) {
+  if (nb <= 8 && dh <= 64 && !general) {
 #define FER_FUSED(NBV)                                                                                       \
   case NBV:                                                                                                  \
     hipLaunchKernelGGL(attn_bwd_fused_bf16<NBV>, dim3(B * H), dim3(64 * NBV), 0, st, (const bf16*)qkv,       \
@@ -845,14 +981,20 @@ extern "C" int fer_attention_bwd(int dtype, const void* qkv, int64_t ld_qkv, con
     part_reduce(ws, B, D3, D3, D3, colsum, nullptr, nullptr, colsum_accumulate, nullptr, st);
     return hip_check("attention_bwd_colsum");
   }
-  FER_NB_SWITCH(nb, hipLaunchKernelGGL(attn_dq_bf16<NB_>, dim3(B * H), dim3(64 * NB_), 0, st, (const bf16*)qkv,
-                                       (long)ld_qkv, (const bf16*)out, (long)ld_out, (const bf16*)dout, (long)ld_dout,
-                                       lse, (bf16*)dqkv, (long)ld_dqkv, N, H, dh, scale, sl2, drop_thresh, drop_scale,
-                                       seed);
-                hipLaunchKernelGGL(attn_dkv_bf16<NB_>, dim3(B * H), dim3(64 * NB_), 0, st, (const bf16*)qkv,
-                                   (long)ld_qkv, (const bf16*)out, (long)ld_out, (const bf16*)dout, (long)ld_dout,
-                                   lse, (bf16*)dqkv, (long)ld_dqkv, N, H, dh, scale, sl2, drop_thresh, drop_scale,
-                                   seed));
+  const dim3 grid(B * H, (N + GEN_ROWS - 1) / GEN_ROWS);
+#define FER_GEN(DH2)                                                                                           \
+  hipLaunchKernelGGL(attn_dq_gen<DH2>, grid, dim3(256), 0, st, (const bf16*)qkv, (long)ld_qkv, (const bf16*)out, \
+                     (long)ld_out, (const bf16*)dout, (long)ld_dout, lse, (bf16*)dqkv, (long)ld_dqkv, N, H, dh,    \
+                     scale, sl2, drop_thresh, drop_scale, seed);                                                \
+  hipLaunchKernelGGL(attn_dkv_gen<DH2>, grid, dim3(256), 0, st, (const bf16*)qkv, (long)ld_qkv, (const bf16*)out, \
+                     (long)ld_out, (const bf16*)dout, (long)ld_dout, lse, (bf16*)dqkv, (long)ld_dqkv, N, H, dh,     \
+                     scale, sl2, drop_thresh, drop_scale, seed);
+  if (dh <= 64) {
+    FER_GEN(1)
+  } else {
+    FER_GEN(2)
+  }
+#undef FER_GEN
   int rc = hip_check("attention_bwd_bf16");
   if (rc || !colsum) return rc;
   return colsum_pass(ws, ws_bytes);

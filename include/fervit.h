@@ -107,7 +107,8 @@ int fer_layernorm_bwd(int dtype, const void* dy, int64_t lddy, const void* x, in
  * probabilities (F.multi_head_attention_forward -> scaled_dot_product_attention inside
  * nn.TransformerEncoderLayer; timm Attention for the hybrid). qkv: [B*N][ld_qkv] with
  * q|k|v column blocks of width H*dh (in_proj rows order); out: [B*N][ld_out].
- * lse [B*H*N] fp32 is saved for backward. bf16: N <= 256, dh <= 64, dh % 8 == 0. */
+ * lse [B*H*N] fp32 is saved for backward. bf16: any N, dh <= 128, dh % 8 == 0 (one workgroup per head
+ * for N <= 256 and dh <= 64, 128-row chunks streamed through LDS otherwise). */
 int64_t fer_attention_ws(int dtype, int B, int N, int H);
 int fer_attention_fwd(int dtype, const void* qkv, int64_t ld_qkv, void* out, int64_t ld_out, float* lse, int B,
                       int N, int H, int dh, float scale, uint32_t drop_thresh, float drop_scale, uint64_t seed,

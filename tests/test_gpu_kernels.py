@@ -210,12 +210,14 @@ def attn_ref(qkv, B, N, H, dh, keep=None, p=0.0):
 
 
 @pytest.mark.parametrize("N,H,dh", [(10, 8, 48), (19, 8, 64), (37, 12, 64), (197, 12, 64), (19, 6, 64), (100, 4, 64),
-                                    (150, 3, 32), (250, 2, 64)])
+                                    (150, 3, 32), (250, 2, 64),
+                                    # general path (csrc/attention.hip attn_*_gen): dh > 64 or N > 256
+                                    (19, 4, 128), (37, 8, 96), (257, 12, 64), (300, 2, 128), (130, 3, 80)])
 @pytest.mark.parametrize("dtype", ["bf16", "fp32"])
 @pytest.mark.parametrize("p", [0.0, 0.1])
 def test_attention_fwd_bwd(N, H, dh, dtype, p):
     o = ops()
-    B = 3 if N == 197 else 8
+    B = 3 if N >= 197 else 8
     D = H * dh
     seed = 4242
     g = torch.Generator().manual_seed(N * 100 + dh)

@@ -31,8 +31,6 @@ def build(name):
 @pytest.mark.parametrize("name", list(CASES))
 @pytest.mark.parametrize("prec", ["fp32", "bf16"])
 def test_model_matches_reference(name, prec):
-    if prec == "bf16" and CASES[name]["ctor"].get("heads", 8) == 4:
-        pytest.skip("bf16 attention kernel covers head_dim <= 64")
     m, fx = build(name)
     m.set_precision(prec)
     m.train()
