@@ -19,6 +19,8 @@
 // fp32 path (parity mode): straightforward kernels over a global [B*H][N][N] workspace.
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "common.h"
 #include "fervit_internal.h"
 
@@ -110,6 +112,19 @@ FER_DEV void img_dma(char* img, __amdgpu_buffer_rsrc_t rs, long row0, long ld, i
   }
 }
 
+// img_dma through the inline-asm LDS-DMA (common.h dma16_asm): for kernels that wait explicitly
+template <int NB>
+FER_DEV void img_dma_asm(char* img, const u32x4& rs, long row0, long ld, int col0, int N, int dh, int w, int lane) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int pc = 4 * w + i;
+    const int r = pc * 8 + (lane >> 3);
+    const int ch = (lane & 7) ^ swz(r);
+    const bool ok = r < N && ch * 8 < dh;
+    dma16_asm(img + pc * 1024, rs, ok ? (uint32_t)(((row0 + r) * ld + col0 + ch * 8) * 2) : FER_OOB);
+  }
+}
+
 FER_DEV void store_rows_q(bf16* o, const f32x16& a0, const f32x16& a1, float mul, int hh, int dh) {
 #pragma unroll
   for (int db = 0; db < 2; ++db)
@@ -135,7 +150,7 @@ __global__ __launch_bounds__(64 * NB) __attribute__((amdgpu_waves_per_eu(4))) vo
   char* Ki = lds;
   char* Vi = lds + NB * 32 * 128;
   const int bh = blockIdx.x, b = bh / H, h = bh - b * H, D = H * dh;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hh = lane >> 5;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), hh = lane >> 5;
   const __amdgpu_buffer_rsrc_t rs = make_rsrc(qkv);
   img_dma<NB>(Ki, rs, (long)b * N, ldq, D + h * dh, N, dh, w, lane);
   img_dma<NB>(Vi, rs, (long)b * N, ldq, 2 * D + h * dh, N, dh, w, lane);
@@ -190,6 +205,172 @@ __global__ __launch_bounds__(64 * NB) __attribute__((amdgpu_waves_per_eu(4))) vo
   if (q < N) {
     store_rows_q(out + ((long)b * N + q) * ldo + h * dh, ot[0], ot[1], 1.f / l, hh, dh);
     if (hh == 0) lse[(long)bh * N + q] = (m + log2f(l)) * LN2;
+  }
+}
+
+// ---------------------------------------------------------------- forward, persistent
+// One workgroup per CU walks the (batch, head) units u = blockIdx.x, + gridDim.x, ...: NB compute
+// waves (wave w = query block w) and one producer wave that DMAs the NEXT unit's K and V images
+// into the other half of a double buffer while the compute waves work on the current unit, so the
+// load phase hides behind the compute phase (one barrier per unit). Compute waves load their next
+// Q fragments at the start of the current unit.
+// Softmax with lazy rescaling: a row's running max m (log2 units) only moves -- and O, l are
+// rescaled -- when a key block's max exceeds it by more than 8 (wave-uniform branch), so
+// P = 2^(s*scale*log2e - m) <= 2^8 and the result is the exact softmax (l uses the same m).
+// Dropout: keep bits hashed as in the other kernels; dscale is applied once per output row instead
+// of once per probability. With `mask` the keep bits are also stored for the backward:
+// mask[((bh*NB + kb)*NB + qb)*32 + j] = bits over the 32 queries of block qb for key kb*32 + j
+// (the ballot of the keep compare of one accumulator register IS such a word for two keys; a
+// wave stores / loads the 32 words of one (kb, qb) tile as one 128-byte row).
+
+// Ballots of the keep compares of accumulator registers R..R+7 (register r: keys acc_row(r, 0)
+// (lanes 0-31) and acc_row(r, 0) + 4 (lanes 32-63)) -> lane k of w takes the 32 query bits of key k
+// (v_writelane_b32). The s_nop: a v_writelane reading an SGPR that a VALU compare wrote in the
+// previous instruction reads the stale value (measured: those keys came back all-zero) and the
+// compiler does not pad inline asm; one nop ahead of 16 writelanes covers all 8 ballots.
+template <int R>
+FER_DEV uint32_t wl_keys8(uint32_t w, const uint64_t* b) {
+  constexpr int k0 = 8 * (R >> 2), k2 = k0 + 2, k4 = k0 + 8, k6 = k0 + 10;
+  asm volatile(
+      "s_nop 4\n\t"
+      "v_writelane_b32 %0, %1, %17\n\tv_writelane_b32 %0, %2, %18\n\t"
+      "v_writelane_b32 %0, %3, %19\n\tv_writelane_b32 %0, %4, %20\n\t"
+      "v_writelane_b32 %0, %5, %21\n\tv_writelane_b32 %0, %6, %22\n\t"
+      "v_writelane_b32 %0, %7, %23\n\tv_writelane_b32 %0, %8, %24\n\t"
+      "v_writelane_b32 %0, %9, %25\n\tv_writelane_b32 %0, %10, %26\n\t"
+      "v_writelane_b32 %0, %11, %27\n\tv_writelane_b32 %0, %12, %28\n\t"
+      "v_writelane_b32 %0, %13, %29\n\tv_writelane_b32 %0, %14, %30\n\t"
+      "v_writelane_b32 %0, %15, %31\n\tv_writelane_b32 %0, %16, %32"
+      : "+v"(w)
+      : "s"((uint32_t)b[0]), "s"((uint32_t)(b[0] >> 32)), "s"((uint32_t)b[1]), "s"((uint32_t)(b[1] >> 32)),
+        "s"((uint32_t)b[2]), "s"((uint32_t)(b[2] >> 32)), "s"((uint32_t)b[3]), "s"((uint32_t)(b[3] >> 32)),
+        "s"((uint32_t)b[4]), "s"((uint32_t)(b[4] >> 32)), "s"((uint32_t)b[5]), "s"((uint32_t)(b[5] >> 32)),
+        "s"((uint32_t)b[6]), "s"((uint32_t)(b[6] >> 32)), "s"((uint32_t)b[7]), "s"((uint32_t)(b[7] >> 32)),
+        "n"(k0), "n"(k0 + 4), "n"(k0 + 1), "n"(k0 + 5), "n"(k2), "n"(k2 + 4), "n"(k2 + 1), "n"(k2 + 5),
+        "n"(k4), "n"(k4 + 4), "n"(k4 + 1), "n"(k4 + 5), "n"(k6), "n"(k6 + 4), "n"(k6 + 1), "n"(k6 + 5));
+  return w;
+}
+
+template <int NB>
+FER_DEV void fwd_dma_unit(char* buf, const u32x4& rs, int unit, long ldq, int N, int H, int dh, int lane) {
+  const int b = unit / H, h = unit - b * H, D = H * dh;
+#pragma unroll 1
+  for (int ww = 0; ww < NB; ++ww) {
+    img_dma_asm<NB>(buf, rs, (long)b * N, ldq, D + h * dh, N, dh, ww, lane);
+    img_dma_asm<NB>(buf + NB * 32 * 128, rs, (long)b * N, ldq, 2 * D + h * dh, N, dh, ww, lane);
+  }
+}
+
+FER_DEV void fwd_load_q(bf16x8 (&qf)[4], const bf16* qkv, long ldq, int unit, int N, int H, int dh, int q, int hh) {
+  const int b = unit / H, h = unit - b * H;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int d0 = 16 * s + 8 * hh;
+    qf[s] = (q < N && d0 < dh) ? *(const bf16x8*)(qkv + ((long)b * N + q) * ldq + h * dh + d0) : bf16x8{};
+  }
+}
+
+template <int NB>
+__global__ __launch_bounds__(64 * (NB + 1)) void attn_fwd_pers(const bf16* __restrict__ qkv, long ldq,
+                                                               bf16* __restrict__ out, long ldo,
+                                                               float* __restrict__ lse, uint32_t* __restrict__ mask,
+                                                               int BH, int N, int H, int dh, float sl2, uint32_t thr,
+                                                               float dscale, uint64_t seed) {
+  seed = step_seed(seed);
+  constexpr int IMG = NB * 32 * 128;
+  __shared__ __attribute__((aligned(1024))) char lds[4 * IMG];  // 2 x (K image, V image)
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), hh = lane >> 5;
+  const u32x4 rs = rsrc4(qkv);
+  const int q = w * 32 + (lane & 31);
+  int u = blockIdx.x;
+  bf16x8 qf[4];
+  if (w == NB) {
+    fwd_dma_unit<NB>(lds, rs, u, ldq, N, H, dh, lane);
+    wait_vm<0>();
+  } else {
+    fwd_load_q(qf, qkv, ldq, u, N, H, dh, q, hh);
+  }
+  bar_lds();
+#pragma unroll 1
+  for (int k = 0;; ++k) {
+    const int un = u + gridDim.x;
+    if (w == NB) {
+      if (un < BH) fwd_dma_unit<NB>(lds + ((k + 1) & 1) * 2 * IMG, rs, un, ldq, N, H, dh, lane);
+      wait_vm<0>();
+    } else {
+      const char* Ki = lds + (k & 1) * 2 * IMG;
+      const char* Vi = Ki + IMG;
+      bf16x8 qn[4];
+      if (un < BH) fwd_load_q(qn, qkv, ldq, un, N, H, dh, q, hh);
+      const int bh = u, b = u / H, h = u - b * H;
+      const uint32_t row = drop_row(bh, N, q);
+      float m = -INFINITY, l = 0.f;
+      f32x16 ot[2] = {f32x16{}, f32x16{}};
+#pragma unroll 1
+      for (int kb = 0; kb < NB; ++kb) {
+        f32x16 st = {};
+#pragma unroll
+        for (int s = 0; s < 4; ++s) st = mfma32(rd_row(Ki, kb * 32 + (lane & 31), 2 * s + hh), qf[s], st);
+        if (kb == NB - 1 && NB * 32 > N) {  // only the last key block has padding keys
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            if (kb * 32 + acc_row(r, hh) >= N) st[r] = -INFINITY;
+        }
+        float bm = fmaxf(fmaxf(st[0], st[1]), st[2]);
+#pragma unroll
+        for (int r = 3; r < 15; r += 2) bm = fmaxf(fmaxf(bm, st[r]), st[r + 1]);
+        bm = fmaxf(bm, st[15]);
+        bm = fmaxf(bm, __shfl_xor(bm, 32, 64)) * sl2;
+        if (__builtin_amdgcn_ballot_w64(bm > m + 8.f)) {  // wave-uniform
+          const float mn = fmaxf(m, bm);
+          const float al = ex2(m - mn);
+          m = mn;
+          l *= al;
+          ot[0] *= al;
+          ot[1] *= al;
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          st[r] = ex2(fmaf(st[r], sl2, -m));
+          l += st[r];
+        }
+        if (thr) {
+          const uint32_t p0 = (row >> 1) + kb * 16 + 2 * hh;  // hash pair of register 0
+          uint64_t bal[16];
+#pragma unroll
+          for (int r = 0; r < 16; r += 2) {
+            const uint32_t hv = fer_hash(seed, p0 + (uint32_t)(acc_row(r, 0) >> 1));
+            const bool k0 = (hv & 0xFFFFu) >= thr, k1 = (hv >> 16) >= thr;
+            st[r] = k0 ? st[r] : 0.f;
+            st[r + 1] = k1 ? st[r + 1] : 0.f;
+            bal[r] = __builtin_amdgcn_ballot_w64(k0);
+            bal[r + 1] = __builtin_amdgcn_ballot_w64(k1);
+          }
+          if (mask) {
+            uint32_t word = 0;
+            word = wl_keys8<0>(word, bal);
+            word = wl_keys8<8>(word, bal + 8);
+            if (lane < 32) mask[(((long)bh * NB + kb) * NB + w) * 32 + lane] = word;
+          }
+        }
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const bf16x8 pf = pack8(st, s2);
+#pragma unroll
+          for (int db = 0; db < 2; ++db) ot[db] = mfma32(rd_tr(Vi, kb * 32 + 16 * s2, db * 32, lane), pf, ot[db]);
+        }
+      }
+      l += __shfl_xor(l, 32, 64);
+      if (q < N) {
+        store_rows_q(out + ((long)b * N + q) * ldo + h * dh, ot[0], ot[1], dscale / l, hh, dh);
+        if (hh == 0) lse[(long)bh * N + q] = (m + log2f(l)) * LN2;
+      }
+#pragma unroll
+      for (int s = 0; s < 4; ++s) qf[s] = qn[s];
+    }
+    bar_lds();  // the producer's DMA of unit un has landed (its wait_vm); every wave is done with unit u
+    u = un;
+    if (u >= BH) break;
   }
 }
 
@@ -251,7 +432,7 @@ __global__ __launch_bounds__(64 * NB) void attn_bwd_fused_bf16(const bf16* __res
   float* lse_s = (float*)(Sall + 2 * NB * 2048);
   float* dd_s = lse_s + NB * 32;
   const int bh = blockIdx.x, b = bh / H, h = bh - b * H, D = H * dh;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hh = lane >> 5;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), hh = lane >> 5;
   img_dma<NB>(Qi, make_rsrc(qkv), (long)b * N, ldq, h * dh, N, dh, w, lane);
   img_dma<NB>(Oi, make_rsrc(dout), (long)b * N, lddo, h * dh, N, dh, w, lane);
   // Dq = rowsum(dO o O): two threads per query row
@@ -450,6 +631,308 @@ __global__ __launch_bounds__(64 * NB) void attn_bwd_fused_bf16(const bf16* __res
   }
 }
 
+// ---------------------------------------------------------------- backward, persistent
+// attn_bwd_fused_bf16's block-pair schedule (wave w = key block w and owner of query block w's
+// dQ; at step i it visits query block (w + i) % NB) in a persistent workgroup per CU that walks
+// the (batch, head) units. While the waves work on unit u, each wave also prepares ITS 32 rows of
+// unit u+1 in the other half of a double buffer, by LDS-DMA only: at step 0 the next dO rows, the
+// next O rows (into the Q slot) and lse; a few steps later (the DMA has landed) Dq = rowsum(dO o O)
+// of those rows from the images, then the next Q rows over the consumed O rows. In the last step
+// the K / V fragments (registers) are reloaded with the next unit's right after their last use.
+// So nothing at a unit boundary waits on HBM latency.
+// Dropout keep bits come from the forward's mask (attn_fwd_pers): one coalesced 128-byte row per
+// (key block, query block) tile. The row's lse enters as the initial accumulator of S
+// (st = S - lse/scale, p = 2^(st * scale * log2e)), so no register holds it.
+// dS tiles are single-buffered (LDS budget), so a step has two barriers: dS written | dQ read.
+// Epilogue (one barrier): dQ^T accumulators stored straight from registers (4 consecutive d per
+// lane = 8-byte pieces), dK / dV staged through the unit's (now free) Q/dO half for 16-byte row
+// stores; in_proj bias-gradient partials per (batch, wave) go straight to `cs_part`
+// ([B][NB][3*D], reduced by part_reduce): dK / dV column sums from the accumulators,
+// colsum(dQ) = K_w^T cs_w with cs_w[k] = sum_q dS[q][k] accumulated over the steps (two MFMAs per
+// 32-column block instead of a cross-lane reduction of the transposed dQ accumulators).
+// LDS (NB = 7): Q/dO images 2 x 56 KB, K images 28 KB, dS tiles 14 KB, lse/Dq 2 x 1.75 KB,
+// cs 0.9 KB = 158.4 KB.
+template <int NB>
+constexpr int pers_bwd_lds_bytes() {
+  return 5 * NB * 4096 + NB * 2048 + 2 * 2 * NB * 32 * 4 + NB * 32 * 4;
+}
+
+template <int NB>
+__global__ __launch_bounds__(64 * NB) void attn_bwd_pers(
+    const bf16* __restrict__ qkv, long ldq, const bf16* __restrict__ out, long ldo, const bf16* __restrict__ dout,
+    long lddo, const float* __restrict__ lse, const uint32_t* __restrict__ mask, bf16* __restrict__ dqkv, long lddq,
+    int BH, int N, int H, int dh, float scale, float sl2, float dscale, float* __restrict__ cs_part, int dbg) {
+  // dbg (FERVIT_ATTN_DBG, timing experiments only): 1 = no step math, 2 = no epilogue stores
+  constexpr int IMG = NB * 32 * 128;
+  constexpr int PREP = NB >= 4 ? 3 : NB - 1;  // step whose dQ phase computes the next unit's Dq
+  __shared__ __attribute__((aligned(1024))) char lds[pers_bwd_lds_bytes<NB>()];
+  char* Kimg = lds + 4 * IMG;               // NB x [32 keys][64 d] images
+  char* Sall = lds + 5 * IMG;               // NB x [32 keys][32 queries] bf16 dS tiles
+  float* lsd = (float*)(Sall + NB * 2048);  // 2 x {L[NB*32] = -lse/scale, Dq[NB*32]}
+  float* csl = lsd + 4 * NB * 32;           // NB x 32: sum_q dS[q][k] of each wave's keys
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), hh = lane >> 5;
+  const int D = H * dh;
+  const int key = w * 32 + (lane & 31);
+  const float inv_scale = 1.f / scale;
+
+  // this wave's 32 rows of `unit`: dO, O (-> Q slot) images and raw lse, by DMA (no wait)
+  auto prep_issue = [&](int unit, int hb) {
+    const int b = unit / H, h = unit - b * H;
+    char* Qi = lds + hb * 2 * IMG;
+    img_dma_asm<NB>(Qi + IMG, rsrc4(dout), (long)b * N, lddo, h * dh, N, dh, w, lane);
+    img_dma_asm<NB>(Qi, rsrc4(out), (long)b * N, ldo, h * dh, N, dh, w, lane);
+    const int r = w * 32 + lane;  // lanes 32..63 would land in the next wave's words: masked off
+    if (lane < 32) dma4_asm(lsd + hb * 2 * NB * 32 + w * 32, rsrc4(lse + (long)unit * N), r < N ? r * 4 : FER_OOB);
+  };
+  // after the DMA landed: L and Dq of this wave's rows, then its Q rows over the consumed O rows
+  auto prep_finish = [&](int unit, int hb) {
+    const int b = unit / H, h = unit - b * H;
+    char* Qi = lds + hb * 2 * IMG;
+    float* L = lsd + hb * 2 * NB * 32;
+    wait_vm<0>();
+    const int r = w * 32 + (lane >> 1), half = lane & 1;  // two lanes per row, 4 chunks each
+    float a = 0.f;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const bf16x8 o = rd_row(Qi, r, 4 * half + c), g = rd_row(Qi + IMG, r, 4 * half + c);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) a = fmaf((float)o[e], (float)g[e], a);
+    }
+    a += __shfl_xor(a, 1, 64);
+    if (!half) {
+      L[NB * 32 + r] = a;
+      L[r] = r < N ? -L[r] * inv_scale : -INFINITY;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // O rows read: Q may land on them
+    img_dma_asm<NB>(Qi, rsrc4(qkv), (long)b * N, ldq, h * dh, N, dh, w, lane);
+  };
+  auto load_frag = [&](bf16x8 (&vq)[4], int unit, int col0) {  // K (col0 = D) / V (2D) row fragments
+    const int b = unit / H, h = unit - b * H;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int d0 = 16 * s + 8 * hh;
+      vq[s] = (key < N && d0 < dh) ? *(const bf16x8*)(qkv + ((long)b * N + key) * ldq + col0 + h * dh + d0)
+                                   : bf16x8{};
+    }
+  };
+  auto write_kimg = [&](const bf16x8 (&kq)[4]) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) *(bf16x8*)(Kimg + w * 4096 + img_off(lane & 31, 2 * s + hh)) = kq[s];
+  };
+  auto mask_word = [&](int unit, int i) -> uint32_t {  // keep word of (key block w, query block (w+i)%NB)
+    int qb = w + i;
+    if (qb >= NB) qb -= NB;
+    return mask ? mask[(((long)unit * NB + w) * NB + qb) * 32 + (lane & 31)] : 0xFFFFFFFFu;
+  };
+
+  int u = blockIdx.x;
+  bf16x8 kf[4], vf[4];
+  prep_issue(u, 0);
+  load_frag(kf, u, D);
+  load_frag(vf, u, 2 * D);
+  uint32_t mwn = mask_word(u, 0);
+  prep_finish(u, 0);
+  write_kimg(kf);
+  wait_vm<0>();
+  bar_lds();
+
+#pragma unroll 1
+  for (int k = 0;; ++k) {
+    const int cur = k & 1, un = u + gridDim.x;
+    const bool has_next = un < BH;
+    const char* Qi = lds + cur * 2 * IMG;
+    const char* Oi = Qi + IMG;
+    const float* L = lsd + cur * 2 * NB * 32;
+    const float* Dq = L + NB * 32;
+    f32x16 dk[2] = {f32x16{}, f32x16{}}, dv[2] = {f32x16{}, f32x16{}};
+    f32x16 dq[2] = {f32x16{}, f32x16{}};  // dQ^T of query block w
+    float cs = 0.f;                       // sum over this lane's query rows of dS[q][key]
+    uint32_t mw0 = 0;                     // keep word of the next unit's first step
+    // one step; the last is a separate instantiation (LAST) so that its extra work -- reloading
+    // kf / vf with the next unit's fragments, the bias-gradient sums -- does not turn every
+    // register it touches into a loop-carried copy
+    auto step = [&](int i, auto last_tag) {
+      constexpr bool LAST = decltype(last_tag)::value;
+      if (!(dbg & 1)) {
+        int lane = threadIdx.x & 63;  // laundered per step: lane-derived LDS addresses are not
+        asm volatile("" : "+v"(lane));  // hoisted out of the step loop (they would pin ~40 VGPRs)
+        const int hh = lane >> 5;
+        if (i == 0 && has_next) prep_issue(un, cur ^ 1);
+        int qb = w + i;
+        if (qb >= NB) qb -= NB;
+        f32x16 st, dp = {};
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {  // S starts at -lse/scale of its 16 query rows
+          const f32x4 l4 = *(const f32x4*)(L + qb * 32 + 8 * g4 + 4 * hh);
+          st[4 * g4] = l4[0];
+          st[4 * g4 + 1] = l4[1];
+          st[4 * g4 + 2] = l4[2];
+          st[4 * g4 + 3] = l4[3];
+        }
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          st = mfma32(rd_row(Qi, qb * 32 + (lane & 31), 2 * s + hh), kf[s], st);
+          dp = mfma32(rd_row(Oi, qb * 32 + (lane & 31), 2 * s + hh), vf[s], dp);
+        }
+        if (LAST && has_next) {  // kf / vf are dead from here on: the next unit's go straight in
+          load_frag(kf, un, D);
+          load_frag(vf, un, 2 * D);
+          mw0 = mask_word(un, 0);
+        }
+        const uint32_t mws = mwn >> (4 * hh);  // bit acc_row(r, 0) = keep of query row r
+        if (i + 1 < NB) mwn = mask_word(u, i + 1);
+        f32x16 pd;
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const f32x4 d4 = *(const f32x4*)(Dq + qb * 32 + 8 * g4 + 4 * hh);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int r = 4 * g4 + j;
+            const float p = ex2(st[r] * sl2);
+            const bool kp = (mws >> acc_row(r, 0)) & 1u;
+            pd[r] = kp ? p : 0.f;
+            st[r] = p * fmaf(kp ? dp[r] : 0.f, dscale, -d4[j]);  // dS
+            cs += st[r];
+          }
+        }
+        char* Si = Sall + w * 2048;
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4)
+          *(bf16x4*)(Si + (lane & 31) * 64 + (8 * g4 + 4 * hh) * 2) =
+              bf16x4{(bf16)st[4 * g4], (bf16)st[4 * g4 + 1], (bf16)st[4 * g4 + 2], (bf16)st[4 * g4 + 3]};
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const bf16x8 pf = pack8(pd, s2), df = pack8(st, s2);
+#pragma unroll
+          for (int db = 0; db < 2; ++db) {
+            dv[db] = mfma32(pf, rd_tr(Oi, qb * 32 + 16 * s2, db * 32, lane), dv[db]);
+            dk[db] = mfma32(df, rd_tr(Qi, qb * 32 + 16 * s2, db * 32, lane), dk[db]);
+          }
+        }
+        if (LAST && cs_part) {  // this wave's keys: sum over all queries of dS
+          cs += __shfl_xor(cs, 32, 64);
+          if (hh == 0) csl[w * 32 + lane] = cs;
+        }
+      }
+      bar_lds();  // every dS tile of this step is in Sall
+      if (!(dbg & 1)) {
+        int lane = threadIdx.x & 63;
+        asm volatile("" : "+v"(lane));
+        const int hh = lane >> 5;
+        int src = w - i;
+        if (src < 0) src += NB;
+        const char* So = Sall + src * 2048;
+        const char* Ko = Kimg + src * 4096;
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const bf16x8 sf = rd_tr64(So, 16 * s2, lane);
+#pragma unroll
+          for (int db = 0; db < 2; ++db) dq[db] = mfma32(rd_tr(Ko, 16 * s2, db * 32, lane), sf, dq[db]);
+        }
+        if (i == PREP && has_next) prep_finish(un, cur ^ 1);
+        if (LAST && cs_part) {
+          // colsum(dQ)[d] over this unit = sum_w K_w^T cs_w: B operand = cs of the wave's keys (k)
+          // in every column (wave-private LDS read-back), A = K_w^T from its image.
+          const int b = u / H, h = u - b * H;
+          const char* Kw = Kimg + w * 4096;
+#pragma unroll
+          for (int db = 0; db < 2; ++db) {
+            f32x16 acc = {};
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) {
+              const f32x4 c0 = *(const f32x4*)(csl + w * 32 + 16 * s2 + 4 * hh);
+              const f32x4 c1 = *(const f32x4*)(csl + w * 32 + 16 * s2 + 8 + 4 * hh);
+              const bf16x8 cf = {(bf16)c0[0], (bf16)c0[1], (bf16)c0[2], (bf16)c0[3],
+                                 (bf16)c1[0], (bf16)c1[1], (bf16)c1[2], (bf16)c1[3]};
+              acc = mfma32(rd_tr(Kw, 16 * s2, db * 32, lane), cf, acc);
+            }
+            if ((lane & 31) == 0) {  // every column holds the same sums: rows d = db*32 + acc_row(r, hh)
+              float* o = cs_part + ((long)b * NB + w) * 3 * D + h * dh + db * 32;
+#pragma unroll
+              for (int g4 = 0; g4 < 4; ++g4) {
+                const int d = 8 * g4 + 4 * hh;
+                if (db * 32 + d < dh)
+                  *(f32x4*)(o + d) = f32x4{acc[4 * g4] * scale, acc[4 * g4 + 1] * scale, acc[4 * g4 + 2] * scale,
+                                           acc[4 * g4 + 3] * scale};
+              }
+            }
+          }
+        }
+      }
+      bar_lds();  // dS tiles and K images read: the next step may overwrite them
+        };
+#pragma unroll 1
+    for (int i = 0; i + 1 < NB; ++i) step(i, std::false_type{});
+    step(NB - 1, std::true_type{});
+    // ---- epilogue of unit u (one barrier)
+    if (has_next) {
+      if (PREP == NB - 1 && (dbg & 1)) prep_finish(un, cur ^ 1);
+      wait_vm<0>();  // this wave's DMA rows of the next unit, its K / V fragments, its mask word
+    }
+    if (!(dbg & 2)) {
+      const int b = u / H, h = u - b * H;
+      const int q = w * 32 + (lane & 31);
+      if (q < N) {  // dQ^T: lane = query, registers = 4 consecutive d per group
+#pragma unroll
+        for (int db = 0; db < 2; ++db)
+#pragma unroll
+          for (int g4 = 0; g4 < 4; ++g4) {
+            const int d = db * 32 + 8 * g4 + 4 * hh;
+            if (d < dh)
+              *(bf16x4*)(dqkv + ((long)b * N + q) * lddq + h * dh + d) =
+                  bf16x4{(bf16)(dq[db][4 * g4] * scale), (bf16)(dq[db][4 * g4 + 1] * scale),
+                         (bf16)(dq[db][4 * g4 + 2] * scale), (bf16)(dq[db][4 * g4 + 3] * scale)};
+          }
+      }
+      if (cs_part) {
+#pragma unroll
+        for (int db = 0; db < 2; ++db) {  // dK / dV column sums over this wave's valid key rows
+          float tk = 0.f, tv = 0.f;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const bool ok = w * 32 + acc_row(r, hh) < N;
+            tk += ok ? dk[db][r] : 0.f;
+            tv += ok ? dv[db][r] : 0.f;
+          }
+          tk += __shfl_xor(tk, 32, 64);
+          tv += __shfl_xor(tv, 32, 64);
+          const int d = db * 32 + (lane & 31);
+          float* o = cs_part + ((long)b * NB + w) * 3 * D + h * dh + d;
+          if (hh == 0 && d < dh) {
+            o[D] = tk * scale;
+            o[2 * D] = tv * dscale;
+          }
+        }
+      }
+      bf16* stg = (bf16*)(lds + cur * 2 * IMG + w * 8192);  // [2][32][64], wave-private (this unit's Q/dO half)
+#pragma unroll
+      for (int db = 0; db < 2; ++db)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int kr = acc_row(r, hh), d = db * 32 + (lane & 31);
+          stg[kr * 64 + d] = (bf16)(dk[db][r] * scale);
+          stg[2048 + kr * 64 + d] = (bf16)(dv[db][r] * dscale);
+        }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int t = i * 64 + lane;  // 512 chunks of 16 B: [2 mats][32 rows][8 chunks]
+        const int mat = t >> 8, kr = (t >> 3) & 31, c = t & 7;
+        const int gk = w * 32 + kr;
+        if (gk < N && c * 8 < dh)
+          *(bf16x8*)(dqkv + ((long)b * N + gk) * lddq + (1 + mat) * D + h * dh + c * 8) =
+              *(const bf16x8*)(stg + mat * 2048 + kr * 64 + c * 8);
+      }
+    }
+    if (has_next) {
+      write_kimg(kf);  // the last step's dQ phase (barrier above) was the last reader of the K images
+      mwn = mw0;
+    }
+    bar_lds();  // next unit: K / Q / dO images (each wave waited for its DMA), L / Dq; staging read
+    u = un;
+    if (!has_next) break;
+  }
+}
+
 // ---------------------------------------------------------------- general path
 // Any N, dh <= 128 (dh % 8 == 0): the head dimension in DH2 halves of 64 columns (each half is
 // one swizzled [rows][128 B] image, so every address helper above is reused unchanged), keys /
@@ -478,7 +961,7 @@ __global__ __launch_bounds__(256) void attn_fwd_gen(const bf16* __restrict__ qkv
   char* Ki = lds;
   char* Vi = lds + DH2 * GEN_IMG;
   const int bh = blockIdx.x, b = bh / H, h = bh - b * H, D = H * dh;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hh = lane >> 5;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), hh = lane >> 5;
   const int q = blockIdx.y * GEN_ROWS + w * 32 + (lane & 31);
   const bool qv = q < N;
   const __amdgpu_buffer_rsrc_t rs = make_rsrc(qkv);
@@ -566,7 +1049,7 @@ __global__ __launch_bounds__(256) void attn_dq_gen(const bf16* __restrict__ qkv,
   char* Ki = lds;
   char* Vi = lds + DH2 * GEN_IMG;
   const int bh = blockIdx.x, b = bh / H, h = bh - b * H, D = H * dh;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hh = lane >> 5;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), hh = lane >> 5;
   const int q = blockIdx.y * GEN_ROWS + w * 32 + (lane & 31);
   const bool qv = q < N;
   const __amdgpu_buffer_rsrc_t rs = make_rsrc(qkv);
@@ -652,7 +1135,7 @@ __global__ __launch_bounds__(256) void attn_dkv_gen(const bf16* __restrict__ qkv
   float* lse_s = (float*)(lds + 2 * DH2 * GEN_IMG);
   float* dd_s = lse_s + GEN_ROWS;
   const int bh = blockIdx.x, b = bh / H, h = bh - b * H, D = H * dh;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hh = lane >> 5;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), hh = lane >> 5;
   const int key = blockIdx.y * GEN_ROWS + w * 32 + (lane & 31);
   const bool kval = key < N;
   bf16x8 kf[4 * DH2], vf[4 * DH2];
@@ -879,15 +1362,35 @@ int fer::set_step_ptr_attention(const uint64_t* p) { return set_step_ptr_here(p)
 extern "C" int64_t fer_attention_ws(int dtype, int B, int N, int H) {
   // fp32 path: P and dS slabs, then the stand-alone colsum pass's partials; bf16: the fused
   // bias-gradient partials [B][3*H*64]
-  const int64_t cs = std::max<int64_t>(fer_colsum_ws(B * N, 3 * H * 128), (int64_t)B * 3 * H * 64 * 4);
+  const int64_t cs = std::max<int64_t>(fer_colsum_ws(B * N, 3 * H * 128), (int64_t)B * 7 * 3 * H * 64 * 4);
   return (dtype == FER_F32 ? (int64_t)2 * B * H * N * N * 4 : 0) + cs;
 }
 
+static bool pers_path(int dtype, int N, int dh) { return dtype == FER_BF16 && N <= 224 && dh <= 64; }
+static int64_t lse_floats(int B, int N, int H) { return ((int64_t)B * H * N + 63) / 64 * 64; }
+static int n_cus() {
+  static const int n = [] {
+    int dev = 0, c = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      c = 256;
+    return c > 0 ? c : 256;
+  }();
+  return n;
+}
+
+extern "C" int64_t fer_attention_saved_floats(int dtype, int B, int N, int H, int dh, uint32_t drop_thresh) {
+  const int64_t nb = (N + 31) / 32;
+  const int64_t mask_words = (drop_thresh && pers_path(dtype, N, dh)) ? (int64_t)B * H * nb * nb * 32 : 0;
+  return lse_floats(B, N, H) + mask_words;
+}
+
 extern "C" int fer_attention_fwd(int dtype, const void* qkv, int64_t ld_qkv, void* out, int64_t ld_out, float* lse,
-                                 int B, int N, int H, int dh, float scale, uint32_t drop_thresh, float drop_scale,
-                                 uint64_t seed, float* ws, int64_t ws_bytes, fer_stream_t stream) {
+                                 int64_t saved_floats, int B, int N, int H, int dh, float scale, uint32_t drop_thresh,
+                                 float drop_scale, uint64_t seed, float* ws, int64_t ws_bytes, fer_stream_t stream) {
   if (B <= 0) return 0;
   hipStream_t st = (hipStream_t)stream;
+  if (saved_floats < fer_attention_saved_floats(dtype, B, N, H, dh, drop_thresh))
+    return set_error("attention_fwd: saved-state buffer smaller than fer_attention_saved_floats()");
   if (dtype == FER_F32) {
     if (!ws || ws_bytes < fer_attention_ws(dtype, B, N, H)) return set_error("attention_fwd: fp32 workspace too small");
     const long pe = (long)B * H * N * N, rows = (long)B * H * N, oe = rows * dh;
@@ -904,11 +1407,26 @@ extern "C" int fer_attention_fwd(int dtype, const void* qkv, int64_t ld_qkv, voi
   if (ld_qkv % 8 || ld_out % 4) return set_error("attention_fwd(bf16): misaligned leading dimension");
   if ((long)B * N * ld_qkv * 2 >= 0x7FFFFFF0L) return set_error("attention_fwd(bf16): qkv exceeds 2 GiB");
   const float sl2 = scale * LOG2E;
-  if (N <= 256 && dh <= 64) {
+  static const bool old_fwd = getenv("FERVIT_ATTN_FWD_OLD") != nullptr;  // A/B switch (no mask: p = 0 only)
+  if (N <= 256 && dh <= 64 && ((old_fwd && !drop_thresh) || N > 224)) {  // NB = 8: 9 waves would not fit 2/SIMD
     const int nb = (N + 31) / 32;
     FER_NB_SWITCH(nb, hipLaunchKernelGGL(attn_fwd_bf16<NB_>, dim3(B * H), dim3(64 * NB_), 0, st, (const bf16*)qkv,
                                          (long)ld_qkv, (bf16*)out, (long)ld_out, lse, N, H, dh, sl2, drop_thresh,
                                          drop_scale, seed));
+  } else if (N <= 224 && dh <= 64) {
+    const int nb = (N + 31) / 32;
+    uint32_t* mask = (drop_thresh && pers_path(dtype, N, dh)) ? (uint32_t*)(lse + lse_floats(B, N, H)) : nullptr;
+    const int grid = std::min(B * H, n_cus());
+#define FER_FPERS(NBV)                                                                                       \
+  case NBV:                                                                                                  \
+    hipLaunchKernelGGL(attn_fwd_pers<NBV>, dim3(grid), dim3(64 * (NBV + 1)), 0, st, (const bf16*)qkv,        \
+                       (long)ld_qkv, (bf16*)out, (long)ld_out, lse, mask, B * H, N, H, dh, sl2, drop_thresh,  \
+                       drop_scale, seed);                                                                   \
+    break;
+    switch (nb) {
+      FER_FPERS(1) FER_FPERS(2) FER_FPERS(3) FER_FPERS(4) FER_FPERS(5) FER_FPERS(6) FER_FPERS(7)
+    }
+#undef FER_FPERS
   } else {
     const dim3 grid(B * H, (N + GEN_ROWS - 1) / GEN_ROWS);
     if (dh <= 64)
@@ -922,12 +1440,14 @@ extern "C" int fer_attention_fwd(int dtype, const void* qkv, int64_t ld_qkv, voi
 }
 
 extern "C" int fer_attention_bwd(int dtype, const void* qkv, int64_t ld_qkv, const void* out, int64_t ld_out,
-                                 const void* dout, int64_t ld_dout, const float* lse, void* dqkv, int64_t ld_dqkv,
-                                 float* ws, int64_t ws_bytes, int B, int N, int H, int dh, float scale,
-                                 uint32_t drop_thresh, float drop_scale, uint64_t seed, float* colsum,
+                                 const void* dout, int64_t ld_dout, const float* lse, int64_t saved_floats, void* dqkv,
+                                 int64_t ld_dqkv, float* ws, int64_t ws_bytes, int B, int N, int H, int dh,
+                                 float scale, uint32_t drop_thresh, float drop_scale, uint64_t seed, float* colsum,
                                  int colsum_accumulate, fer_stream_t stream) {
   if (B <= 0) return 0;
   hipStream_t st = (hipStream_t)stream;
+  if (saved_floats < fer_attention_saved_floats(dtype, B, N, H, dh, drop_thresh))
+    return set_error("attention_bwd: saved-state buffer smaller than fer_attention_saved_floats()");
   const int D3 = 3 * H * dh;
   if (colsum && (!ws || ws_bytes < fer_attention_ws(dtype, B, N, H)))
     return set_error("attention_bwd: colsum needs the workspace (fer_attention_ws bytes)");
@@ -963,6 +1483,26 @@ extern "C" int fer_attention_bwd(int dtype, const void* qkv, int64_t ld_qkv, con
   const float sl2 = scale * LOG2E;
   static const bool general = getenv("FERVIT_ATTN_GENERAL") != nullptr;  // A/B switch: general path only
   static const int dbg = getenv("FERVIT_ATTN_DBG") ? atoi(getenv("FERVIT_ATTN_DBG")) : 0;  // timing experiments
+  static const bool old_bwd = getenv("FERVIT_ATTN_BWD_OLD") != nullptr;  // A/B switch (p = 0 only)
+  if (pers_path(dtype, N, dh) && !general && !(old_bwd && !drop_thresh)) {
+    const uint32_t* mask = drop_thresh ? (const uint32_t*)(lse + lse_floats(B, N, H)) : nullptr;
+    const int grid = std::min(B * H, n_cus());
+#define FER_PERS(NBV)                                                                                          \
+  case NBV:                                                                                                    \
+    hipLaunchKernelGGL(attn_bwd_pers<NBV>, dim3(grid), dim3(64 * NBV), 0, st, (const bf16*)qkv,                \
+                       (long)ld_qkv, (const bf16*)out, (long)ld_out, (const bf16*)dout, (long)ld_dout, lse, mask, \
+                       (bf16*)dqkv, (long)ld_dqkv, B * H, N, H, dh, scale, sl2, drop_scale, colsum ? ws : nullptr, \
+                       dbg);                                                                                     \
+    break;
+    switch (nb) {
+      FER_PERS(1) FER_PERS(2) FER_PERS(3) FER_PERS(4) FER_PERS(5) FER_PERS(6) FER_PERS(7)
+    }
+#undef FER_PERS
+    int rc = hip_check("attention_bwd_bf16_pers");
+    if (rc || !colsum) return rc;
+    part_reduce(ws, B * nb, D3, D3, D3, colsum, nullptr, nullptr, colsum_accumulate, nullptr, st);
+    return hip_check("attention_bwd_colsum");
+  }
   if (nb <= 8 && dh <= 64 && !general) {
 #define FER_FUSED(NBV)                                                                                       \
   case NBV:                                                                                                  \

@@ -210,6 +210,37 @@ FER_DEV void wait_vm() {
 
 // mask out-of-tile lanes by giving them FER_OOB as voffset.
 #define FER_OOB 0x80000000u
+
+// Buffer descriptor as four dwords (same fields as make_rsrc) for the inline-asm LDS-DMA below.
+FER_DEV u32x4 rsrc4(const void* base) {
+  const uint64_t a = (uint64_t)base;
+  return u32x4{(uint32_t)a, (uint32_t)(a >> 32) & 0xFFFFu, 0x7FFFFFF0u, 0x00020000u};
+}
+FER_DEV uint32_t lds_addr(const void* p) { return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p; }
+// LDS-DMA (buffer_load ... lds; lane l's 16 or 4 bytes land at lds + 16*l / 4*l) issued by inline
+// asm: the compiler's wait-count pass does not see the LDS write, so it neither pads every later
+// LDS read with s_waitcnt vmcnt(0) (it cannot tell the DMA target from the other LDS data) nor
+// orders anything against it -- the issuing wave waits (wait_vm) before the data is read.
+// s_nop: an SALU write of M0 needs one wait state before an LDS-DMA reads it. M0 is reserved by the
+// compiler (a clobber is not honoured), so the asm saves and restores it.
+FER_DEV void dma16_asm(const void* lds, const u32x4& rs, uint32_t voff) {
+  uint32_t t;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dwordx4 %2, %3, 0 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(t) : "s"(lds_addr(lds)), "v"(voff), "s"(rs) : "memory");
+}
+FER_DEV void dma4_asm(const void* lds, const u32x4& rs, uint32_t voff) {
+  uint32_t t;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dword %2, %3, 0 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(t) : "s"(lds_addr(lds)), "v"(voff), "s"(rs) : "memory");
+}
+// Workgroup barrier for LDS data only: no vmcnt(0) (__syncthreads' release fence waits for every
+// outstanding global load and store of the wave -- prefetches and stores would be exposed at
+// every barrier). Data that arrived by LDS-DMA must be waited for by its issuing wave first.
+FER_DEV void bar_lds() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 FER_DEV __amdgpu_buffer_rsrc_t make_rsrc(const void* base) {
   return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)0x7FFFFFF0, 0x00020000);
 }

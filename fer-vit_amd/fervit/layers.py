@@ -95,7 +95,7 @@ class PostNormLayerFn(torch.autograd.Function):
         f32 = torch.float32
         qkv = ops.linear_fwd(x, _weight(flat, in_w, dt), in_b.data)
         o = _empty(M, D, x)
-        lse = torch.empty(cfg.B * cfg.H * cfg.N, dtype=f32, device=x.device)
+        lse = ops.attention_saved(qkv, cfg.B, cfg.N, cfg.H, dh, dropout=pd)
         ops.attention_fwd(qkv, o, lse, cfg.B, cfg.N, cfg.H, dh, dropout=pd, seed=seeds[0])
         y = ops.linear_fwd(o, _weight(flat, out_w, dt), out_b.data, res=x, dropout=pd, seed=seeds[1], drop_ld=D)
         m1 = torch.empty(M, dtype=f32, device=x.device)
@@ -176,7 +176,7 @@ class PreNormBlockFn(torch.autograd.Function):
         h1 = ops.layernorm_fwd(x, n1w.data, n1b.data, cfg.eps, mean=m1, rstd=r1)
         qkv = ops.linear_fwd(h1, _weight(flat, qkv_w, dt), qkv_b.data)
         o = _empty(M, D, x)
-        lse = torch.empty(cfg.B * cfg.H * cfg.N, dtype=f32, device=x.device)
+        lse = ops.attention_saved(qkv, cfg.B, cfg.N, cfg.H, dh)
         ops.attention_fwd(qkv, o, lse, cfg.B, cfg.N, cfg.H, dh)
         x2 = ops.linear_fwd(o, _weight(flat, proj_w, dt), proj_b.data, res=x)
         m2 = torch.empty(M, dtype=f32, device=x.device)

@@ -186,17 +186,27 @@ def layernorm_bwd(dy, x, mean, rstd, w, dx=None, res=None, dx_drop=None, dropout
 
 
 # ------------------------------------------------------------------ attention
-def attention_fwd(qkv, out, lse, B, N, H, dh, dropout=0.0, seed=0):
+def attention_saved(qkv, B, N, H, dh, dropout=0.0) -> torch.Tensor:
+    """fp32 buffer for the state fer_attention_fwd keeps for the backward: lse [B*H*N] first
+    (`saved[:B*H*N]`), then the dropout keep bits of the fast bf16 path."""
+    thr, _ = drop_args(dropout)
+    n = lib().fer_attention_saved_floats(dcode(qkv), B, N, H, dh, thr)
+    return torch.empty(n, dtype=torch.float32, device=qkv.device)
+
+
+def attention_fwd(qkv, out, saved, B, N, H, dh, dropout=0.0, seed=0):
+    """out = attention(qkv); `saved` from attention_saved() (same B, N, H, dh, dropout)."""
     thr, sc = drop_args(dropout)
     nb = lib().fer_attention_ws(dcode(qkv), B, N, H)
     ws = WS.get(nb, qkv.device) if nb else None
     check(lib().fer_attention_fwd(dcode(qkv), qkv.data_ptr(), qkv.stride(0), out.data_ptr(), out.stride(0),
-                                  lse.data_ptr(), B, N, H, dh, 1.0 / math.sqrt(dh), thr, sc, seed & (2**64 - 1),
-                                  ptr(ws), 0 if ws is None else ws.numel() * 4, stream()), "attention_fwd")
+                                  saved.data_ptr(), saved.numel(), B, N, H, dh, 1.0 / math.sqrt(dh), thr, sc,
+                                  seed & (2**64 - 1), ptr(ws), 0 if ws is None else ws.numel() * 4, stream()),
+          "attention_fwd")
     return out
 
 
-def attention_bwd(qkv, out, dout, lse, dqkv, B, N, H, dh, dropout=0.0, seed=0, colsum=None,
+def attention_bwd(qkv, out, dout, saved, dqkv, B, N, H, dh, dropout=0.0, seed=0, colsum=None,
                   colsum_accumulate=False):
     """dqkv = d(attention)/d(qkv); colsum (fp32 [3*H*dh], optional) (+)= column sums of dqkv
     (the in_proj bias gradient), fused into the backward kernel."""
@@ -204,7 +214,8 @@ def attention_bwd(qkv, out, dout, lse, dqkv, B, N, H, dh, dropout=0.0, seed=0, c
     nb = lib().fer_attention_ws(dcode(qkv), B, N, H)
     ws = WS.get(nb, qkv.device) if nb else None
     check(lib().fer_attention_bwd(dcode(qkv), qkv.data_ptr(), qkv.stride(0), out.data_ptr(), out.stride(0),
-                                  dout.data_ptr(), dout.stride(0), lse.data_ptr(), dqkv.data_ptr(), dqkv.stride(0),
+                                  dout.data_ptr(), dout.stride(0), saved.data_ptr(), saved.numel(), dqkv.data_ptr(),
+                                  dqkv.stride(0),
                                   ptr(ws), 0 if ws is None else ws.numel() * 4, B, N, H, dh, 1.0 / math.sqrt(dh),
                                   thr, sc, seed & (2**64 - 1), ptr(colsum), int(colsum_accumulate), stream()),
           "attention_bwd")

@@ -107,19 +107,25 @@ int fer_layernorm_bwd(int dtype, const void* dy, int64_t lddy, const void* x, in
  * probabilities (F.multi_head_attention_forward -> scaled_dot_product_attention inside
  * nn.TransformerEncoderLayer; timm Attention for the hybrid). qkv: [B*N][ld_qkv] with
  * q|k|v column blocks of width H*dh (in_proj rows order); out: [B*N][ld_out].
- * lse [B*H*N] fp32 is saved for backward. bf16: any N, dh <= 128, dh % 8 == 0 (one workgroup per head
- * for N <= 256 and dh <= 64, 128-row chunks streamed through LDS otherwise). */
+ * `saved` (saved_floats fp32 words, >= fer_attention_saved_floats(...)) is the state kept for the
+ * backward: lse [B*H*N] (natural log), padded to a multiple of 64 words, then -- bf16 with dropout,
+ * N <= 224, dh <= 64 -- the probability-dropout keep bits, [B*H][NB][NB][32] uint32 (NB = ceil(N/32);
+ * word (kb, qb, j) = bits over the 32 queries of block qb for key kb*32 + j), so the backward does
+ * not re-hash them. bf16: any N, dh <= 128, dh % 8 == 0 (persistent workgroup per CU walking the
+ * (batch, head) units for N <= 256 and dh <= 64, 128-row chunks streamed through LDS otherwise). */
 int64_t fer_attention_ws(int dtype, int B, int N, int H);
-int fer_attention_fwd(int dtype, const void* qkv, int64_t ld_qkv, void* out, int64_t ld_out, float* lse, int B,
-                      int N, int H, int dh, float scale, uint32_t drop_thresh, float drop_scale, uint64_t seed,
-                      float* ws, int64_t ws_bytes, fer_stream_t stream);
+int64_t fer_attention_saved_floats(int dtype, int B, int N, int H, int dh, uint32_t drop_thresh);
+int fer_attention_fwd(int dtype, const void* qkv, int64_t ld_qkv, void* out, int64_t ld_out, float* saved,
+                      int64_t saved_floats, int B, int N, int H, int dh, float scale, uint32_t drop_thresh,
+                      float drop_scale, uint64_t seed, float* ws, int64_t ws_bytes, fer_stream_t stream);
 /* Backward: dqkv [B*N][ld_dqkv] (dq|dk|dv). Optional colsum [3*H*dh] fp32 (+)= column sums of
  * dqkv over the B*N rows = in_proj.bias gradient, fused into the kernel (per-(batch) partials
  * + fixed-order reduction). ws >= fer_attention_ws bytes (fp32 path scratch / colsum partials). */
 int fer_attention_bwd(int dtype, const void* qkv, int64_t ld_qkv, const void* out, int64_t ld_out,
-                      const void* dout, int64_t ld_dout, const float* lse, void* dqkv, int64_t ld_dqkv, float* ws,
-                      int64_t ws_bytes, int B, int N, int H, int dh, float scale, uint32_t drop_thresh,
-                      float drop_scale, uint64_t seed, float* colsum, int colsum_accumulate, fer_stream_t stream);
+                      const void* dout, int64_t ld_dout, const float* saved, int64_t saved_floats, void* dqkv,
+                      int64_t ld_dqkv, float* ws, int64_t ws_bytes, int B, int N, int H, int dh, float scale,
+                      uint32_t drop_thresh, float drop_scale, uint64_t seed, float* colsum, int colsum_accumulate,
+                      fer_stream_t stream);
 
 /* Column sums: out[n] (+)= scale * sum_m x[m][n]  (bias gradients). ws >= fer_colsum_ws(M,N). */
 int64_t fer_colsum_ws(int M, int N);

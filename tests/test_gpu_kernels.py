@@ -4,6 +4,8 @@ tight). Dropout masks are rebuilt on the host from the kernel's hash (tests/drop
 so dropout paths are checked element-exactly too."""
 import math
 
+import numpy as np
+
 import pytest
 import torch
 
@@ -227,18 +229,30 @@ def test_attention_fwd_bwd(N, H, dh, dtype, p):
     tol = 2e-2 if dtype == "bf16" else 1e-4
     qd = cast(qkv)
     out = torch.empty(B * N, D, device=DEV, dtype=qd.dtype)
-    lse = torch.empty(B * H * N, device=DEV)
-    o.attention_fwd(qd, out, lse, B, N, H, dh, dropout=p, seed=seed)
+    saved = o.attention_saved(qd, B, N, H, dh, dropout=p)
+    lse = saved[:B * H * N]
+    o.attention_fwd(qd, out, saved, B, N, H, dh, dropout=p, seed=seed)
     # attention dropout index: (bh*N + q)*NP + k, NP = N rounded up to even (csrc/attention.hip)
     keep = keep_mask(seed, (B, H, N, N + (N & 1)), p)[..., :N] if p > 0 else None
     qr = qd.float().cpu().requires_grad_(True)
     ref, lse_ref = attn_ref(qr, B, N, H, dh, keep, p)
     assert rel_err(out.cpu(), ref) < tol
     assert (lse.cpu() - lse_ref.reshape(-1)).abs().max().item() < (2e-2 if dtype == "bf16" else 1e-4)
+    nb = (N + 31) // 32
+    if p > 0 and saved.numel() > B * H * N + 63:
+        # persistent bf16 path: keep bits stored for the backward, word (kb, qb, j) = bits over the
+        # 32 queries of block qb for key kb*32 + j (csrc/attention.hip attn_fwd_pers)
+        off = (B * H * N + 63) // 64 * 64
+        words = saved[off:off + B * H * nb * nb * 32].view(torch.int32).cpu().numpy().view(np.uint32)
+        words = words.reshape(B * H, nb, nb, 32).astype(np.uint64)
+        bits = (words[..., None] >> np.arange(32, dtype=np.uint64)) & np.uint64(1)  # [bh][kb][qb][j][qi]
+        got = torch.from_numpy(bits.transpose(0, 2, 4, 1, 3).reshape(B * H, nb * 32, nb * 32).astype(bool))
+        want = keep.reshape(B * H, N, N)
+        assert torch.equal(got[:, :N, :N], want)
     dd = cast(dout)
     dqkv = torch.empty_like(qd)
     cs = torch.full((3 * D,), 0.5, device=DEV)  # fused in_proj.bias gradient, accumulated
-    o.attention_bwd(qd, out, dd, lse, dqkv, B, N, H, dh, dropout=p, seed=seed, colsum=cs, colsum_accumulate=True)
+    o.attention_bwd(qd, out, dd, saved, dqkv, B, N, H, dh, dropout=p, seed=seed, colsum=cs, colsum_accumulate=True)
     ref.backward(dd.float().cpu())
     assert rel_err(cs.cpu() - 0.5, qr.grad.sum(0)) < 2 * tol
     for j, name in enumerate("qkv"):
@@ -248,7 +262,7 @@ def test_attention_fwd_bwd(N, H, dh, dtype, p):
     # deterministic: a second backward reproduces every bit (fixed-order dQ / bias sums)
     dqkv2 = torch.empty_like(qd)
     cs2 = torch.full((3 * D,), 0.5, device=DEV)
-    o.attention_bwd(qd, out, dd, lse, dqkv2, B, N, H, dh, dropout=p, seed=seed, colsum=cs2, colsum_accumulate=True)
+    o.attention_bwd(qd, out, dd, saved, dqkv2, B, N, H, dh, dropout=p, seed=seed, colsum=cs2, colsum_accumulate=True)
     assert torch.equal(dqkv2, dqkv) and torch.equal(cs2, cs)
 
 

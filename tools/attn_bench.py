@@ -22,13 +22,13 @@ def main():
     g = torch.Generator(device=dev).manual_seed(0)
     qkv = torch.randn(M, 3 * D, device=dev, generator=g).to(torch.bfloat16)
     out = torch.empty(M, D, device=dev, dtype=torch.bfloat16)
-    lse = torch.empty(B * H * N, device=dev)
     dout = torch.randn(M, D, device=dev, generator=g).to(torch.bfloat16)
     dqkv = torch.empty(M, 3 * D, device=dev, dtype=torch.bfloat16)
     fl_f = 4.0 * N * N * dh * B * H
     by_f = 2.0 * M * 4 * D
     by_b = 2.0 * M * 8 * D
     for p in (0.1, 0.0):
+        lse = ops.attention_saved(qkv, B, N, H, dh, dropout=p)
         tf = min(timeit(lambda: ops.attention_fwd(qkv, out, lse, B, N, H, dh, dropout=p, seed=5)) for _ in range(3))
         tb = min(timeit(lambda: ops.attention_bwd(qkv, out, dout, lse, dqkv, B, N, H, dh, dropout=p, seed=5))
                  for _ in range(3))
