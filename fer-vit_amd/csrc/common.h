@@ -22,7 +22,10 @@ typedef __attribute__((ext_vector_type(16))) float f32x16;
 typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
 typedef __attribute__((address_space(3))) void lds_void;
 
-enum { FER_ACT_NONE = 0, FER_ACT_GELU = 1, FER_ACT_RELU = 2 };
+enum { FER_ACT_NONE = 0, FER_ACT_GELU = 1, FER_ACT_RELU = 2, FER_ACT_MUL = 3 /* aux_act only: v *= aux */ };
+// act flag: `pre` receives the backward GATE act'(v) * keep * drop_scale instead of the
+// pre-activation v (the input-gradient GEMM then only multiplies by it: aux_act = FER_ACT_MUL).
+enum { FER_PRE_GATE = 16 };
 
 FER_DEV float bf2f(bf16 x) { return (float)x; }
 FER_DEV bf16 f2bf(float x) { return (bf16)x; }
@@ -132,11 +135,30 @@ FER_DEV f32x2 gelu_erf_grad2(f32x2 x) {  // packed gelu_erf_grad, same arithmeti
   const f32x2 cdf = 0.5f * (1.0f + __builtin_elementwise_copysign(r, z));
   return __builtin_elementwise_fma(x * 0.39894228040143268f, e, cdf);
 }
+// GELU and its derivative together, packed: erf by Abramowitz-Stegun 7.1.26 from e = exp(-x^2/2),
+// which is also the derivative's pdf term -- one exponential and one reciprocal per element for
+// both (|erf error| <= 1.5e-7).
+FER_DEV f32x2 gelu_and_grad2(f32x2 x, f32x2& grad) {
+  const f32x2 h = -0.5f * x * x;
+  const f32x2 e = f32x2{__expf(h[0]), __expf(h[1])};
+  const f32x2 z = x * 0.70710678118654752f;
+  const f32x2 d = __builtin_elementwise_fma(kpk(0.3275911f), __builtin_elementwise_abs(z), f32x2(1.0f));
+  const f32x2 t = f32x2{__builtin_amdgcn_rcpf(d[0]), __builtin_amdgcn_rcpf(d[1])};
+  f32x2 y = __builtin_elementwise_fma(kpk(1.061405429f), t, kpk(-1.453152027f));
+  y = __builtin_elementwise_fma(y, t, kpk(1.421413741f));
+  y = __builtin_elementwise_fma(y, t, kpk(-0.284496736f));
+  y = __builtin_elementwise_fma(y, t, kpk(0.254829592f));
+  const f32x2 r = 1.0f - y * t * e;
+  const f32x2 cdf = 0.5f * (1.0f + __builtin_elementwise_copysign(r, z));
+  grad = __builtin_elementwise_fma(x * 0.39894228040143268f, e, cdf);
+  return x * cdf;
+}
 FER_DEV float act_fwd(int act, float x) {
   return act == FER_ACT_GELU ? gelu_erf(x) : (act == FER_ACT_RELU ? fmaxf(x, 0.f) : x);
 }
 FER_DEV float act_grad(int act, float x) {
-  return act == FER_ACT_GELU ? gelu_erf_grad(x) : (act == FER_ACT_RELU ? (x > 0.f ? 1.f : 0.f) : 1.f);
+  return act == FER_ACT_GELU ? gelu_erf_grad(x)
+                             : (act == FER_ACT_RELU ? (x > 0.f ? 1.f : 0.f) : (act == FER_ACT_MUL ? x : 1.f));
 }
 
 // ---------------------------------------------------------------- dropout RNG
@@ -176,6 +198,12 @@ FER_DEV bool drop_keep(uint64_t seed, uint32_t idx, uint32_t thresh) {
   if (thresh == 0u) return true;
   const uint32_t h = fer_hash(seed, idx >> 1);
   return ((h >> ((idx & 1) * 16)) & 0xFFFFu) >= thresh;
+}
+// Keep bits of 4 consecutive elements starting at an even index (two hashes): bit r = element r.
+FER_DEV uint32_t keep4(uint64_t seed, uint32_t idx, uint32_t thresh) {
+  const uint32_t h0 = fer_hash(seed, idx >> 1), h1 = fer_hash(seed, (idx >> 1) + 1);
+  return (uint32_t)((h0 & 0xFFFFu) >= thresh) | ((uint32_t)((h0 >> 16) >= thresh) << 1) |
+         ((uint32_t)((h1 & 0xFFFFu) >= thresh) << 2) | ((uint32_t)((h1 >> 16) >= thresh) << 3);
 }
 // 4 consecutive elements starting at an even index: two hashes.
 FER_DEV void drop4(uint64_t seed, uint32_t idx, uint32_t thresh, float scale, f32x4& v) {

@@ -42,26 +42,46 @@ FER_DEV bf16x8 pack8(f32x4 a, f32x4 b) {
 }
 FER_DEV void epi8_bf16(const EpiArgs& e, long m, long n, f32x4& v0, f32x4& v1, f32x4 b0, f32x4 b1, bf16x8 x,
                        float ps, uint64_t seed) {
+  const int act = e.act & 15;
+  const bool gate = (e.act & FER_PRE_GATE) && e.pre;
   v0 = v0 * e.alpha + b0;
   v1 = v1 * e.alpha + b1;
-  if (e.pre) *(bf16x8*)((bf16*)e.pre + m * e.ldp + n) = pack8(v0, v1);
-  if (e.act == FER_ACT_GELU) {
-    v0.xy = gelu_erf_fast2(v0.xy);
-    v0.zw = gelu_erf_fast2(v0.zw);
-    v1.xy = gelu_erf_fast2(v1.xy);
-    v1.zw = gelu_erf_fast2(v1.zw);
-  } else if (e.act == FER_ACT_RELU) {
+  if (e.pre && !gate) *(bf16x8*)((bf16*)e.pre + m * e.ldp + n) = pack8(v0, v1);
+  f32x4 g0 = f32x4{1.f, 1.f, 1.f, 1.f}, g1 = g0;  // gate act'(pre), when `pre` receives it
+  if (act == FER_ACT_GELU) {
+    if (gate) {
+      f32x2 t;
+      v0.xy = gelu_and_grad2(v0.xy, t); g0.xy = t;
+      v0.zw = gelu_and_grad2(v0.zw, t); g0.zw = t;
+      v1.xy = gelu_and_grad2(v1.xy, t); g1.xy = t;
+      v1.zw = gelu_and_grad2(v1.zw, t); g1.zw = t;
+    } else {
+      v0.xy = gelu_erf_fast2(v0.xy);
+      v0.zw = gelu_erf_fast2(v0.zw);
+      v1.xy = gelu_erf_fast2(v1.xy);
+      v1.zw = gelu_erf_fast2(v1.zw);
+    }
+  } else if (act == FER_ACT_RELU) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
+      g0[r] = v0[r] > 0.f ? 1.f : 0.f;
+      g1[r] = v1[r] > 0.f ? 1.f : 0.f;
       v0[r] = fmaxf(v0[r], 0.f);
       v1[r] = fmaxf(v1[r], 0.f);
     }
   }
   if (e.drop_thresh) {
     const uint32_t idx = (uint32_t)m * (uint32_t)e.drop_ld + (uint32_t)n;
-    drop4(seed, idx, e.drop_thresh, e.drop_scale, v0);
-    drop4(seed, idx + 4, e.drop_thresh, e.drop_scale, v1);
+    const uint32_t k = keep4(seed, idx, e.drop_thresh) | (keep4(seed, idx + 4, e.drop_thresh) << 4);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      v0[r] = (k >> r) & 1 ? v0[r] * e.drop_scale : 0.f;
+      v1[r] = (k >> (4 + r)) & 1 ? v1[r] * e.drop_scale : 0.f;
+      g0[r] = (k >> r) & 1 ? g0[r] * e.drop_scale : 0.f;
+      g1[r] = (k >> (4 + r)) & 1 ? g1[r] * e.drop_scale : 0.f;
+    }
   }
+  if (gate) *(bf16x8*)((bf16*)e.pre + m * e.ldp + n) = pack8(g0, g1);
   if (e.post_scale) {
     v0 *= ps;
     v1 *= ps;
@@ -69,7 +89,10 @@ FER_DEV void epi8_bf16(const EpiArgs& e, long m, long n, f32x4& v0, f32x4& v1, f
   if (e.aux) {
     const bf16x8 a = e.res ? *(const bf16x8*)((const bf16*)e.aux + m * e.ldx + n) : x;
     const f32x4 a0 = lo4(a), a1 = hi4(a);
-    if (e.aux_act == FER_ACT_GELU) {
+    if (e.aux_act == FER_ACT_MUL) {
+      v0 *= a0;
+      v1 *= a1;
+    } else if (e.aux_act == FER_ACT_GELU) {
       v0.xy *= gelu_erf_grad2(a0.xy);
       v0.zw *= gelu_erf_grad2(a0.zw);
       v1.xy *= gelu_erf_grad2(a1.xy);
@@ -107,14 +130,28 @@ FER_DEV void epi8_bf16(const EpiArgs& e, long m, long n, f32x4& v0, f32x4& v1, f
 
 template <typename T>
 FER_DEV void epi4(const EpiArgs& e, long m, long n, f32x4 v, uint64_t seed) {
+  const int act = e.act & 15;
+  const bool gate = (e.act & FER_PRE_GATE) && e.pre;
   v *= e.alpha;
   if (e.bias) v += *(const f32x4*)(e.bias + n);
-  if (e.pre) store4<T>((T*)e.pre + m * e.ldp + n, v);
-  if (e.act) {
+  if (e.pre && !gate) store4<T>((T*)e.pre + m * e.ldp + n, v);
+  f32x4 gt = f32x4{1.f, 1.f, 1.f, 1.f};
+  if (act) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) v[r] = act_fwd(e.act, v[r]);
+    for (int r = 0; r < 4; ++r) {
+      if (gate) gt[r] = act_grad(act, v[r]);
+      v[r] = act_fwd(act, v[r]);
+    }
   }
-  if (e.drop_thresh) drop4(seed, (uint32_t)m * (uint32_t)e.drop_ld + (uint32_t)n, e.drop_thresh, e.drop_scale, v);
+  if (e.drop_thresh) {
+    const uint32_t k = keep4(seed, (uint32_t)m * (uint32_t)e.drop_ld + (uint32_t)n, e.drop_thresh);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      v[r] = (k >> r) & 1 ? v[r] * e.drop_scale : 0.f;
+      gt[r] = (k >> r) & 1 ? gt[r] * e.drop_scale : 0.f;
+    }
+  }
+  if (gate) store4<T>((T*)e.pre + m * e.ldp + n, gt);
   if (e.post_scale) v *= *e.post_scale;
   if (e.aux) {
     f32x4 a = load4<T>((const T*)e.aux + m * e.ldx + n);
@@ -646,6 +683,83 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_ring_kernel(GemmArgs g, 
   tile_epilogue<BM, BN, WM, WN, MT, EPC, NST * STAGE>(g, e, acc, smem, m0, n0, ks, wm, wn, lane);
 }
 
+// ===================================================================== ping-pong kernel
+// 256x128 tile on 4 waves (2 x 2, each a 128x64 accumulator tile of 16x16 blocks), BK=32 stages in
+// a 3-slot LDS ring (72 KB): small enough for TWO workgroups per CU, so one workgroup's epilogue
+// (VALU: bias, GELU, dropout hashing; LDS staging; stores) runs beside the other's MFMA main loop
+// instead of idling the matrix pipe. One barrier per K-step: it publishes stage t (every wave
+// waited for its own DMA pieces of it) and releases slot (t-1)%3, which is refilled with stage
+// t+2 right after it (two K-steps of DMA slack). Fragments of a K-step are read after the
+// barrier; the partner workgroup's waves fill the SIMD while they land.
+template <bool AKC, bool BKC>
+__global__ __launch_bounds__(256, 2) void gemm_pp_kernel(GemmArgs g, EpiArgs e) {
+  typedef f32x4 AccT;
+  constexpr int BM = 256, BN = 128, WM = 2, WN = 2, MT = 16, RBK = 32, NST = 3, NW = 4;
+  constexpr int TM = BM / WM, TN = BN / WN, FM = TM / MT, FN = TN / MT;
+  constexpr int A_BYTES = BM * RBK * 2, B_BYTES = BN * RBK * 2, STAGE = A_BYTES + B_BYTES;
+  __shared__ __attribute__((aligned(1024))) char smem[NST * STAGE];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave % WM, wn = wave / WM;
+  int tm, tn;
+  tile_of(blockIdx.x, g.tiles_m, g.tiles_n, tm, tn);
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int ks = blockIdx.y;
+  const int kbeg = ks * g.k_chunk;
+  const int kend = min(g.K, kbeg + g.k_chunk);
+  const int nk = (kend - kbeg + RBK - 1) / RBK;
+  const int ktail = kbeg + (nk - 1) * RBK;
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(g.A);
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(g.B);
+  typedef DmaPlan<BM, AKC, NW, MT, RBK> PA;
+  typedef DmaPlan<BN, BKC, NW, MT, RBK> PB;
+  PA pa;
+  PB pb;
+  pa.init(wave, lane, g.lda, m0, g.M);
+  pb.init(wave, lane, g.ldb, n0, g.N);
+  constexpr int PER = PA::NI + PB::NI;  // DMA instructions per stage per wave
+  auto slot = [&](int st) -> char* { return smem + (st % NST) * STAGE; };
+  auto issue = [&](int st) {
+    const int k0 = kbeg + st * RBK;
+    pa.issue(ra, slot(st), wave, g.lda, k0, kend, k0 == ktail);
+    pb.issue(rb, slot(st) + A_BYTES, wave, g.ldb, k0, kend, k0 == ktail);
+  };
+  AccT acc[FN][FM];
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int j = 0; j < FM; ++j) acc[i][j] = AccT{};
+  if (nk > 0) issue(0);
+  if (nk > 1) issue(1);
+  for (int t = 0; t < nk; ++t) {
+    if (t + 1 < nk) wait_vm<PER>();  // stage t landed (own pieces); stage t+1 may fly
+    else wait_vm<0>();
+    __builtin_amdgcn_s_barrier();   // stage t published; slot (t-1)%3 free
+    asm volatile("" ::: "memory");
+    if (t + 2 < nk) issue(t + 2);
+    const char* cur = slot(t);
+    bf16x8 af[FM], bfr[FN];
+#pragma unroll
+    for (int i = 0; i < FN; ++i) bfr[i] = read_frag<MT, BN, BKC, RBK>(cur + A_BYTES, wn * TN + i * MT, 0, lane);
+#pragma unroll
+    for (int j = 0; j < FM; ++j) af[j] = read_frag<MT, BM, AKC, RBK>(cur, wm * TM + j * MT, 0, lane);
+#pragma unroll
+    for (int j = 0; j < FM; ++j)
+#pragma unroll
+      for (int i = 0; i < FN; ++i) acc[i][j] = mfma<MT>(bfr[i], af[j], acc[i][j]);
+  }
+  __syncthreads();  // every wave's fragment reads are done: the ring becomes epilogue staging
+  tile_epilogue<BM, BN, WM, WN, MT, 2, NST * STAGE>(g, e, acc, smem, m0, n0, ks, wm, wn, lane);
+}
+
+template <bool AKC, bool BKC>
+static int launch_pp(GemmArgs g, const EpiArgs& e, hipStream_t st) {
+  g.tiles_m = (g.M + 255) / 256;
+  g.tiles_n = (g.N + 127) / 128;
+  hipLaunchKernelGGL((gemm_pp_kernel<AKC, BKC>), dim3(g.tiles_m * g.tiles_n, g.splits), dim3(256), 0, st, g, e);
+  return 0;
+}
+
 // ===================================================================== 8-phase kernel
 // 256x256x64 tile, 8 waves as 2 (row halves, wr = wave>>2) x 4 (column quarters, wc = wave&3),
 // each wave a 128x64 accumulator tile cut into four 64x32 quadrants. A K-tile runs as four
@@ -992,8 +1106,9 @@ static int forced_cfg() {
 }
 
 // Tile configuration: 0..3 double-buffered (256^2 MT32, 256^2 MT16, 128^2 MT32, 128^2 MT16),
-// 4..7 BK=32 ring (same order), 8/9 the 8-phase 256^2 kernel (MT16 / MT32).
-static bool cfg_is_256(int c) { return c == 0 || c == 1 || c == 4 || c == 5 || c == 8 || c == 9; }
+// 4..7 BK=32 ring (same order), 8/9 the 8-phase 256^2 kernel (MT16 / MT32), 10 the ping-pong
+// 256x128 kernel (two workgroups per CU).
+static bool cfg_is_256(int c) { return c == 0 || c == 1 || c == 4 || c == 5 || c == 8 || c == 9 || c == 10; }
 
 template <bool AKC, bool BKC>
 static int dispatch_tile(int cfg, GemmArgs g, const EpiArgs& e, hipStream_t st) {
@@ -1007,6 +1122,7 @@ static int dispatch_tile(int cfg, GemmArgs g, const EpiArgs& e, hipStream_t st) 
     case 6: return launch_ring<128, 128, 2, 2, AKC, BKC, 32>(g, e, st);
     case 7: return launch_ring<128, 128, 2, 2, AKC, BKC, 16>(g, e, st);
     case 9: return launch_8ph<AKC, BKC, 32>(g, e, st);
+    case 10: return launch_pp<AKC, BKC>(g, e, st);
     default: return launch_8ph<AKC, BKC, 16>(g, e, st);
   }
 }
@@ -1108,7 +1224,7 @@ extern "C" int64_t fer_gemm_colsum_ws(int M, int N) {
 }
 
 extern "C" int fer_gemm_set_config(int cfg) {
-  if (cfg < -1 || cfg > 9) return fer::set_error("gemm_set_config: cfg must be -1 (automatic) or 0..9");
+  if (cfg < -1 || cfg > 10) return fer::set_error("gemm_set_config: cfg must be -1 (automatic) or 0..10");
   fer::g_forced_cfg = cfg;
   return 0;
 }

@@ -102,8 +102,10 @@ class PostNormLayerFn(torch.autograd.Function):
         r1 = torch.empty_like(m1)
         x1 = ops.layernorm_fwd(y, n1w.data, n1b.data, cfg.eps, mean=m1, rstd=r1)
         f = _empty(M, F, x) if cfg.save else None
-        g = ops.linear_fwd(x1, _weight(flat, w1, dt), b1.data, pre=f, act=cfg.act, dropout=pd, seed=seeds[2],
-                           drop_ld=F)
+        # f = the backward gate act'(pre) * keep / (1 - p) of linear1's output: the linear2 dgrad
+        # below applies GELU' and the dropout in one multiply
+        g = ops.linear_fwd(x1, _weight(flat, w1, dt), b1.data, pre=f, pre_gate=True, act=cfg.act, dropout=pd,
+                           seed=seeds[2], drop_ld=F)
         z = ops.linear_fwd(g, _weight(flat, w2, dt), b2.data, res=x1, dropout=pd, seed=seeds[3], drop_ld=D)
         m2 = torch.empty(M, dtype=f32, device=x.device)
         r2 = torch.empty_like(m2)
@@ -135,8 +137,7 @@ class PostNormLayerFn(torch.autograd.Function):
         if gw2 is not None:
             ops.linear_wgrad(dh2, g, gw2, accumulate=acc)
         # linear1.bias grad = column sums of dF, fused into this GEMM's epilogue
-        dF = _dgrad(flat, dh2, w2, dt, dropout=pd, seed=seeds[2], drop_ld=w1.shape[0], aux=f,
-                              aux_act=cfg.act, colsum=gb1, colsum_accumulate=acc)
+        dF = _dgrad(flat, dh2, w2, dt, aux=f, aux_act="mul", colsum=gb1, colsum_accumulate=acc)
         if gw1 is not None:
             ops.linear_wgrad(dF, x1, gw1, accumulate=acc)
         dx1 = _dgrad(flat, dF, w1, dt, res=dz)
@@ -183,7 +184,7 @@ class PreNormBlockFn(torch.autograd.Function):
         r2 = torch.empty_like(m2)
         h2 = ops.layernorm_fwd(x2, n2w.data, n2b.data, cfg.eps, mean=m2, rstd=r2)
         f = _empty(M, F, x) if cfg.save else None
-        g = ops.linear_fwd(h2, _weight(flat, fc1_w, dt), fc1_b.data, pre=f, act="gelu")
+        g = ops.linear_fwd(h2, _weight(flat, fc1_w, dt), fc1_b.data, pre=f, pre_gate=True, act="gelu")
         out = ops.linear_fwd(g, _weight(flat, fc2_w, dt), fc2_b.data, res=x2)
         if cfg.save:
             ctx.cfg, ctx.flat, ctx.P = cfg, flat, P
@@ -206,8 +207,7 @@ class PreNormBlockFn(torch.autograd.Function):
             ops.colsum(dout, gfc2_b, accumulate=acc)
         if gfc2_w is not None:
             ops.linear_wgrad(dout, g, gfc2_w, accumulate=acc)
-        dF = _dgrad(flat, dout, fc2_w, dt, aux=f, aux_act="gelu", colsum=gfc1_b,
-                              colsum_accumulate=acc)
+        dF = _dgrad(flat, dout, fc2_w, dt, aux=f, aux_act="mul", colsum=gfc1_b, colsum_accumulate=acc)
         if gfc1_w is not None:
             ops.linear_wgrad(dF, h2, gfc1_w, accumulate=acc)
         dh2 = _dgrad(flat, dF, fc1_w, dt)
@@ -238,7 +238,7 @@ class AdapterFn(torch.autograd.Function):
         A = fc1_w.shape[0]
         dt = x.dtype
         u = _empty(M, A, x) if cfg.save else None
-        v = ops.linear_fwd(x, _weight(flat, fc1_w, dt), fc1_b.data, pre=u, act="gelu")
+        v = ops.linear_fwd(x, _weight(flat, fc1_w, dt), fc1_b.data, pre=u, pre_gate=True, act="gelu")
         T = _empty(M, D, x) if cfg.save else None
         out = ops.linear_fwd(v, _weight(flat, fc2_w, dt), fc2_b.data, pre=T, post_scale=alpha.data, res=x)
         if cfg.save:
@@ -263,7 +263,7 @@ class AdapterFn(torch.autograd.Function):
             ops.colsum(dout, g2b, accumulate=acc, scale=a)
         if g2w is not None:
             ops.linear_wgrad(dout, v, g2w, accumulate=acc, post_scale=a)
-        du = _dgrad(flat, dout, fc2_w, dt, post_scale=a, aux=u, aux_act="gelu")
+        du = _dgrad(flat, dout, fc2_w, dt, post_scale=a, aux=u, aux_act="mul")
         if g1b is not None:
             ops.colsum(du, g1b, accumulate=acc)
         if g1w is not None:

@@ -14,7 +14,8 @@ import torch
 from . import _lib
 from ._lib import Epilogue, GemmDesc, check, lib
 
-ACT = {"none": 0, "gelu": 1, "relu": 2}
+ACT = {"none": 0, "gelu": 1, "relu": 2, "mul": 3}  # "mul": aux_act only (v *= aux)
+PRE_GATE = 16  # act flag: `pre` receives act'(pre) * keep * drop_scale (include/fervit.h)
 
 # Optional callable(desc, epilogue, launch) used by bench.py to bracket launches with HIP events.
 LAUNCH_PROBE = None
@@ -78,9 +79,11 @@ def gemm(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, *, a_kc: bool = Tr
          res: Optional[torch.Tensor] = None, dropout: float = 0.0, seed: int = 0, drop_ld: Optional[int] = None,
          aux: Optional[torch.Tensor] = None, aux_act: str = "none", alpha: float = 1.0, accumulate: bool = False,
          post_scale: Optional[torch.Tensor] = None, split_ws: bool = True,
-         colsum: Optional[torch.Tensor] = None, colsum_accumulate: bool = False) -> torch.Tensor:
+         colsum: Optional[torch.Tensor] = None, colsum_accumulate: bool = False,
+         pre_gate: bool = False) -> torch.Tensor:
     """out[m][n] = epilogue(sum_k A(m,k) B(n,k)); see include/fervit.h for the layouts.
-    colsum: optional fp32 [N] receiving (or, with colsum_accumulate, adding) sum_m out[m][n]."""
+    colsum: optional fp32 [N] receiving (or, with colsum_accumulate, adding) sum_m out[m][n].
+    pre_gate: `pre` receives act'(pre) * dropout keep * scale (consumed by aux_act="mul")."""
     _dev(A)
     if A.dtype != B.dtype:
         raise TypeError("gemm: A and B dtypes differ")
@@ -107,7 +110,7 @@ def gemm(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, *, a_kc: bool = Tr
     e.accumulate = int(accumulate)
     e.alpha = alpha
     e.bias = ptr(bias)
-    e.act = ACT[act]
+    e.act = ACT[act] | (PRE_GATE if pre_gate else 0)
     e.pre = ptr(pre)
     e.ldp = N if pre is None else pre.stride(0)
     e.res = ptr(res)

@@ -38,7 +38,8 @@ extern "C" {
 typedef struct ihipStream_t* fer_stream_t; /* == hipStream_t */
 
 enum { FER_BF16 = 0, FER_F32 = 1 };
-enum { FER_ACT_NONE_ = 0, FER_ACT_GELU_ = 1, FER_ACT_RELU_ = 2 };
+enum { FER_ACT_NONE_ = 0, FER_ACT_GELU_ = 1, FER_ACT_RELU_ = 2, FER_ACT_MUL_ = 3 /* aux_act only */ };
+enum { FER_PRE_GATE_ = 16 /* act flag, see fer_epilogue */ };
 
 /* C = epilogue(sum_k A(m,k) B(n,k)); A(m,k) = a_kc ? A[m*lda+k] : A[k*lda+m],
  * B(n,k) = b_kc ? B[n*ldb+k] : B[k*ldb+n].
@@ -55,7 +56,10 @@ typedef struct {
 
 /* Epilogue, applied per element in this order:
  *   v = alpha*acc (+ bias[n]); pre[m][n] = v; v = act(v); v = dropout(v, seed, m*drop_ld+n);
- *   v *= *post_scale; v *= act'(aux[m][n]); v += res[m][n]; c[m][n] (+)= v            */
+ *   v *= *post_scale; v *= act'(aux[m][n]); v += res[m][n]; c[m][n] (+)= v
+ * act | FER_PRE_GATE_: pre[m][n] receives the backward gate act'(v) * keep * drop_scale (the
+ * same keep bit as v's dropout) instead of v; the input-gradient GEMM of the next layer then
+ * applies act' and the dropout in one multiply with aux_act = FER_ACT_MUL_ (v *= aux[m][n]). */
 typedef struct {
   void* c; int64_t ldc; int c_f32; int accumulate; float alpha;
   const float* bias; int act;

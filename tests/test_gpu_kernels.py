@@ -92,7 +92,7 @@ def test_gemm_persistent_many_tiles(M, N, K):
     assert torch.equal(yd != 0, keep)
 
 
-@pytest.mark.parametrize("cfg", list(range(10)))
+@pytest.mark.parametrize("cfg", list(range(11)))
 def test_gemm_every_tile_config(cfg):
     """Each bf16 kernel configuration (forced through fer_gemm_set_config) on ragged shapes,
     all three operand layouts, split-K, and the fused epilogue."""
@@ -146,6 +146,38 @@ def test_gemm_epilogue_bias_act_dropout_residual(act):
     aa.backward(torch.where(keep, dG / (1 - p), torch.zeros(())))
     assert rel_err(dF.cpu(), hh.grad) < 2e-2
     assert rel_err(cs.cpu(), hh.grad.sum(0)) < 2e-2
+
+
+@pytest.mark.parametrize("act", ["gelu", "relu"])
+@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_gemm_pre_gate_and_mul(act, dtype, p):
+    """pre_gate: `pre` receives act'(h) * keep / (1 - p) (the same keep bits as the output's
+    dropout); the FFN input-gradient GEMM then multiplies by it (aux_act="mul") -- equal to the
+    dropout + act' epilogue of test_gemm_epilogue_bias_act_dropout_residual (csrc/gemm.hip)."""
+    o = ops()
+    M, N, K, seed = 1030, 640, 384, 2468
+    g = torch.Generator().manual_seed(7)
+    x, w = torch.randn(M, K, generator=g), torch.randn(N, K, generator=g) / math.sqrt(K)
+    b = torch.randn(N, generator=g)
+    cast = bf if dtype == "bf16" else (lambda t: t.to(DEV))
+    tol = 1e-2 if dtype == "bf16" else 1e-5
+    gate = torch.empty(M, N, device=DEV, dtype=cast(x).dtype)
+    y = o.linear_fwd(cast(x), cast(w), b.to(DEV), pre=gate, pre_gate=True, act=act, dropout=p, seed=seed)
+    xr, wr = cast(x).float().cpu(), cast(w).float().cpu()
+    hh = (xr @ wr.t() + b).requires_grad_(True)
+    a = torch.nn.functional.gelu(hh) if act == "gelu" else torch.relu(hh)
+    keep = keep_mask(seed, (M, N), p) if p > 0 else torch.ones(M, N, dtype=torch.bool)
+    assert rel_err(y.cpu(), torch.where(keep, a / (1 - p), torch.zeros(()))) < tol
+    a.backward(torch.ones_like(a))
+    assert rel_err(gate.cpu(), torch.where(keep, hh.grad / (1 - p), torch.zeros(()))) < tol
+    dy = torch.randn(M, K, generator=g)
+    w2 = torch.randn(K, N, generator=g) / math.sqrt(N)
+    cs = torch.zeros(N, device=DEV)
+    dF = o.linear_dgrad(cast(dy), cast(w2), aux=gate, aux_act="mul", colsum=cs)
+    ref = (cast(dy).float().cpu() @ cast(w2).float().cpu()) * gate.float().cpu()
+    assert rel_err(dF.cpu(), ref) < 2 * tol
+    assert rel_err(cs.cpu(), ref.sum(0)) < 2 * tol
 
 
 def test_gemm_keep_rate():

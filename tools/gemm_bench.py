@@ -44,6 +44,8 @@ def main():
         "fc1 fwd plain": (lambda: ops.linear_fwd(x, w1), 2 * M * F * D, lambda: x @ w1.t()),
         "fc1 fwd +bias+gelu+drop+pre": (lambda: ops.linear_fwd(x, w1, b1, pre=pre, act="gelu", dropout=0.1, seed=7),
                                          2 * M * F * D, None),
+        "fc1 fwd +bias+gelu+drop+gate": (lambda: ops.linear_fwd(x, w1, b1, pre=pre, pre_gate=True, act="gelu",
+                                                                 dropout=0.1, seed=7), 2 * M * F * D, None),
         "fc1 fwd +bias": (lambda: ops.linear_fwd(x, w1, b1, out=out_f), 2 * M * F * D, None),
         "fc1 fwd +bias+gelu": (lambda: ops.linear_fwd(x, w1, b1, out=out_f, act="gelu"), 2 * M * F * D, None),
         "fc1 fwd +bias+relu+pre": (lambda: ops.linear_fwd(x, w1, b1, out=out_f, act="relu", pre=pre), 2 * M * F * D, None),
@@ -55,6 +57,8 @@ def main():
         "fc2 dgrad (B KC, W^T copy)": (lambda: ops.linear_fwd(x, w2t, out=out_f), 2 * M * F * D, None),
         "fc2 dgrad fused (B MN)": (lambda: ops.linear_dgrad(x, w2, out=out_f, **fused), 2 * M * F * D, None),
         "fc2 dgrad fused (B KC)": (lambda: ops.linear_fwd(x, w2t, out=out_f, **fused), 2 * M * F * D, None),
+        "fc2 dgrad gate-mul (B KC)": (lambda: ops.linear_fwd(x, w2t, out=out_f, aux=pre, aux_act="mul", colsum=cs),
+                                      2 * M * F * D, None),
         "fc1 dgrad +res (B MN, K=3072)": (lambda: ops.linear_dgrad(h, w1, out=out_d, res=x), 2 * M * F * D, None),
         "fc1 dgrad +res (B KC, K=3072)": (lambda: ops.linear_fwd(h, w1t, out=out_d, res=x), 2 * M * F * D, None),
         "fc1 wgrad (MN,MN splitK)": (lambda: ops.linear_wgrad(dF, x, gw), 2 * M * F * D, lambda: dF.t() @ x),
