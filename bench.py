@@ -143,8 +143,10 @@ class GemmProbe:
         a.record(s)
         r = launch()
         b.record(s)
-        parts = [n for n, on in (("bias", e.bias), ("gelu" if e.act == 1 else "relu", e.act), ("drop", e.drop_thresh),
-                                 ("pre", e.pre), ("act'", e.aux), ("res", e.res), ("colsum", e.colsum)) if on]
+        act, gate = e.act & 15, bool(e.act & 16)
+        parts = [n for n, on in (("bias", e.bias), ("gelu" if act == 1 else "relu", act), ("drop", e.drop_thresh),
+                                 ("gate" if gate else "pre", e.pre), ("x gate" if e.aux_act == 3 else "act'", e.aux),
+                                 ("res", e.res), ("colsum", e.colsum)) if on]
         kind = "epi:" + ("+".join(parts) or "none")
         self.rec.append(((d.M, d.N, d.K), kind, 2.0 * d.M * d.N * d.K, gemm_algo_bytes(d, e), a, b))
         return r
