@@ -306,11 +306,25 @@ __global__ __launch_bounds__(64 * (NB + 1)) void attn_fwd_pers(const bf16* __res
       const uint32_t row = drop_row(bh, N, q);
       float m = -INFINITY, l = 0.f;
       f32x16 ot[2] = {f32x16{}, f32x16{}};
+      // software pipeline: the next key block's K fragments and this block's V fragments are read
+      // from LDS before the softmax math, so their latency hides behind it
+      bf16x8 kfr[4];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) kfr[s] = rd_row(Ki, lane & 31, 2 * s + hh);
 #pragma unroll 1
       for (int kb = 0; kb < NB; ++kb) {
         f32x16 st = {};
 #pragma unroll
-        for (int s = 0; s < 4; ++s) st = mfma32(rd_row(Ki, kb * 32 + (lane & 31), 2 * s + hh), qf[s], st);
+        for (int s = 0; s < 4; ++s) st = mfma32(kfr[s], qf[s], st);
+        if (kb + 1 < NB) {
+#pragma unroll
+          for (int s = 0; s < 4; ++s) kfr[s] = rd_row(Ki, (kb + 1) * 32 + (lane & 31), 2 * s + hh);
+        }
+        bf16x8 vfr[2][2];
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+          for (int db = 0; db < 2; ++db) vfr[s2][db] = rd_tr(Vi, kb * 32 + 16 * s2, db * 32, lane);
         if (kb == NB - 1 && NB * 32 > N) {  // only the last key block has padding keys
 #pragma unroll
           for (int r = 0; r < 16; ++r)
@@ -357,7 +371,7 @@ __global__ __launch_bounds__(64 * (NB + 1)) void attn_fwd_pers(const bf16* __res
         for (int s2 = 0; s2 < 2; ++s2) {
           const bf16x8 pf = pack8(st, s2);
 #pragma unroll
-          for (int db = 0; db < 2; ++db) ot[db] = mfma32(rd_tr(Vi, kb * 32 + 16 * s2, db * 32, lane), pf, ot[db]);
+          for (int db = 0; db < 2; ++db) ot[db] = mfma32(vfr[s2][db], pf, ot[db]);
         }
       }
       l += __shfl_xor(l, 32, 64);
