@@ -6,6 +6,8 @@
 // the norm (post-norm `LN(x + Drop(h))` -> d h = Drop'(d(x+Drop h))), and the
 // per-column partial sums for dgamma, dbeta and the branch bias gradient, reduced
 // afterwards in fixed block order (deterministic).
+#include <stdlib.h>
+
 #include "common.h"
 #include "fervit_internal.h"
 
@@ -151,6 +153,195 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, l
   }
 }
 
+// ---------------------------------------------------------------- bf16, 16-byte rows
+// Half-wave (32 lanes) per row, 8 consecutive columns (one 16-byte piece) per lane and chunk,
+// CPL = ceil(D / 256) chunks: half the memory instructions of the 4-wide kernels above; the forward
+// keeps two rows in flight per half-wave (the next row's loads issued before the current row's
+// stores).
+FER_DEV f32x4 lo4b(bf16x8 x) { return f32x4{(float)x[0], (float)x[1], (float)x[2], (float)x[3]}; }
+FER_DEV f32x4 hi4b(bf16x8 x) { return f32x4{(float)x[4], (float)x[5], (float)x[6], (float)x[7]}; }
+FER_DEV bf16x8 pk8(f32x4 a, f32x4 b) {
+  return bf16x8{(bf16)a[0], (bf16)a[1], (bf16)a[2], (bf16)a[3], (bf16)b[0], (bf16)b[1], (bf16)b[2], (bf16)b[3]};
+}
+FER_DEV float half_sum(float v) {  // sum over the 32 lanes of this half-wave
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <int CPL>
+__global__ __launch_bounds__(256) void ln_fwd8_kernel(const bf16* __restrict__ x, long ldx, const float* __restrict__ g,
+                                                      const float* __restrict__ b, int grows, int rdiv,
+                                                      bf16* __restrict__ y, long ldy, float* __restrict__ mean,
+                                                      float* __restrict__ rstd, int M, int D, float eps) {
+  const int l32 = threadIdx.x & 31;
+  const long hw = (long)blockIdx.x * 8 + (threadIdx.x >> 5);  // this half-wave's first row
+  const long stride = (long)gridDim.x * 8;
+  const int nc = D >> 3;
+  bf16x8 va[CPL], vb[CPL];
+  auto load = [&](long row, bf16x8(&v)[CPL]) {
+#pragma unroll
+    for (int i = 0; i < CPL; ++i) {
+      const int c = l32 + 32 * i;
+      v[i] = (row < M && c < nc) ? *(const bf16x8*)(x + row * ldx + c * 8) : bf16x8{};
+    }
+  };
+  auto proc = [&](long row, const bf16x8(&v)[CPL]) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < CPL; ++i) {
+      const f32x4 a = lo4b(v[i]), c = hi4b(v[i]);
+      s += (a[0] + a[1]) + (a[2] + a[3]) + (c[0] + c[1]) + (c[2] + c[3]);
+    }
+    const float mu = half_sum(s) / D;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < CPL; ++i) {
+      if (l32 + 32 * i < nc) {
+        const f32x4 a = lo4b(v[i]) - mu, c = hi4b(v[i]) - mu;
+        q += a[0] * a[0] + a[1] * a[1] + a[2] * a[2] + a[3] * a[3] + c[0] * c[0] + c[1] * c[1] + c[2] * c[2] +
+             c[3] * c[3];
+      }
+    }
+    const float rs = rsqrtf(half_sum(q) / D + eps);
+    const long gr = grows > 1 ? ((row / rdiv) % grows) * D : 0;
+#pragma unroll
+    for (int i = 0; i < CPL; ++i) {
+      const int c = l32 + 32 * i;
+      if (c < nc) {
+        const float* gp = g + gr + c * 8;
+        const float* bp = b + gr + c * 8;
+        const f32x4 o0 = (lo4b(v[i]) - mu) * rs * *(const f32x4*)gp + *(const f32x4*)bp;
+        const f32x4 o1 = (hi4b(v[i]) - mu) * rs * *(const f32x4*)(gp + 4) + *(const f32x4*)(bp + 4);
+        *(bf16x8*)(y + row * ldy + c * 8) = pk8(o0, o1);
+      }
+    }
+    if (l32 == 0) {
+      if (mean) mean[row] = mu;
+      if (rstd) rstd[row] = rs;
+    }
+  };
+  long row = hw;
+  load(row, va);
+  for (; row < M; row += 2 * stride) {
+    const long r2 = row + stride;
+    load(r2, vb);
+    proc(row, va);
+    if (r2 >= M) break;
+    load(r2 + stride, va);
+    proc(r2, vb);
+  }
+}
+
+// partial layout as ln_bwd_kernel: ws[blk][3][D]
+template <int CPL>
+__global__ __launch_bounds__(256) void ln_bwd8_kernel(const bf16* __restrict__ dy, long lddy, const bf16* __restrict__ x,
+                                                      long ldx, const float* __restrict__ mean,
+                                                      const float* __restrict__ rstd, const float* __restrict__ g,
+                                                      int grows, int rdiv, const bf16* __restrict__ res, long ldr,
+                                                      bf16* __restrict__ dx, long lddx, bf16* __restrict__ dxd,
+                                                      uint32_t thr, float dscale, uint64_t seed,
+                                                      float* __restrict__ part, int want_part, int M, int D) {
+  seed = step_seed(seed);
+  const int l32 = threadIdx.x & 31, hwi = threadIdx.x >> 5;
+  const long stride = (long)gridDim.x * 8;
+  const int nc = D >> 3;
+  f32x4 pg[CPL][2], pb[CPL][2], pd[CPL][2];
+#pragma unroll
+  for (int i = 0; i < CPL; ++i)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) pg[i][h] = pb[i][h] = pd[i][h] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 dyA[CPL], xA[CPL], rA[CPL];
+  auto load = [&](long row, bf16x8(&dyr)[CPL], bf16x8(&xr)[CPL], bf16x8(&rr)[CPL]) {
+#pragma unroll
+    for (int i = 0; i < CPL; ++i) {
+      const int c = l32 + 32 * i;
+      const bool ok = row < M && c < nc;
+      dyr[i] = ok ? *(const bf16x8*)(dy + row * lddy + c * 8) : bf16x8{};
+      xr[i] = ok ? *(const bf16x8*)(x + row * ldx + c * 8) : bf16x8{};
+      if (res) rr[i] = ok ? *(const bf16x8*)(res + row * ldr + c * 8) : bf16x8{};
+    }
+  };
+  auto proc = [&](long row, const bf16x8(&dyr)[CPL], const bf16x8(&xr)[CPL], const bf16x8(&rr)[CPL]) {
+    const float mu = mean[row], rs = rstd[row];
+    const long gr = grows > 1 ? ((row / rdiv) % grows) * D : 0;
+    // pass 1: the two row sums (xhat and dy*gamma are recomputed in pass 2: registers, not VALU,
+    // bound this kernel's occupancy)
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < CPL; ++i) {
+      const int c = l32 + 32 * i;
+      if (c < nc) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const f32x4 dv = h ? hi4b(dyr[i]) : lo4b(dyr[i]);
+          const f32x4 xh = ((h ? hi4b(xr[i]) : lo4b(xr[i])) - mu) * rs;
+          const f32x4 gy = dv * *(const f32x4*)(g + gr + c * 8 + 4 * h);
+          const f32x4 t = gy * xh;
+          s1 += (gy[0] + gy[1]) + (gy[2] + gy[3]);
+          s2 += (t[0] + t[1]) + (t[2] + t[3]);
+          pg[i][h] += dv * xh;
+          pb[i][h] += dv;
+        }
+      }
+    }
+    s1 = half_sum(s1) / D;
+    s2 = half_sum(s2) / D;
+#pragma unroll
+    for (int i = 0; i < CPL; ++i) {
+      const int c = l32 + 32 * i;
+      if (c < nc) {
+        f32x4 d[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const f32x4 xh = ((h ? hi4b(xr[i]) : lo4b(xr[i])) - mu) * rs;
+          const f32x4 gy = (h ? hi4b(dyr[i]) : lo4b(dyr[i])) * *(const f32x4*)(g + gr + c * 8 + 4 * h);
+          d[h] = (gy - s1 - xh * s2) * rs;
+          if (res) d[h] += h ? hi4b(rr[i]) : lo4b(rr[i]);
+        }
+        *(bf16x8*)(dx + row * lddx + c * 8) = pk8(d[0], d[1]);
+        if (dxd) {
+          const uint32_t idx = (uint32_t)row * (uint32_t)D + (uint32_t)(c * 8);
+          const uint32_t k = thr ? (keep4(seed, idx, thr) | (keep4(seed, idx + 4, thr) << 4)) : 0xFFu;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            d[0][r] = (k >> r) & 1 ? d[0][r] * dscale : 0.f;
+            d[1][r] = (k >> (4 + r)) & 1 ? d[1][r] * dscale : 0.f;
+          }
+          *(bf16x8*)(dxd + row * lddx + c * 8) = pk8(d[0], d[1]);
+        }
+        pd[i][0] += d[0];
+        pd[i][1] += d[1];
+      }
+    }
+  };
+  // one row at a time per half-wave (the column partials take the registers a second row set would
+  // need; occupancy hides the load latency)
+  for (long row = (long)blockIdx.x * 8 + hwi; row < M; row += stride) {
+    load(row, dyA, xA, rA);
+    proc(row, dyA, xA, rA);
+  }
+  if (!want_part) return;
+  // column partials: 8 half-waves of the block (same columns), fixed order through LDS
+  __shared__ float red[8][CPL * 256];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    if (k) __syncthreads();
+#pragma unroll
+    for (int i = 0; i < CPL; ++i)
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        *(f32x4*)&red[hwi][(l32 + 32 * i) * 8 + 4 * h] = k == 0 ? pg[i][h] : (k == 1 ? pb[i][h] : pd[i][h]);
+    __syncthreads();
+    for (int c = threadIdx.x; c < D; c += 256) {
+      float t = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) t += red[j][c];
+      part[((long)blockIdx.x * 3 + k) * D + c] = t;
+    }
+  }
+}
+
 // out_k[col] (+)= sum_blk part[blk][k][col] for k in {0,1,2}
 __global__ __launch_bounds__(256) void ln_part_reduce_kernel(const float* __restrict__ part, int nblk, int D,
                                                              float* o0, float* o1, float* o2, int accumulate) {
@@ -180,7 +371,20 @@ extern "C" int fer_layernorm_fwd(int dtype, const void* x, int64_t ldx, const fl
   if (gamma_rows < 1) gamma_rows = 1;
   if (row_div < 1) row_div = 1;
   dim3 grid(ceil_div(M, 4));
-  if (dtype == FER_BF16)
+  static const bool old_ln = getenv("FERVIT_LN_OLD") != nullptr;  // A/B switch
+  if (dtype == FER_BF16 && D % 8 == 0 && ldx % 8 == 0 && ldy % 8 == 0 && !old_ln) {
+    const dim3 g8(std::max(1, std::min(ceil_div(M, 16), 2048)));  // two rows per half-wave in flight
+#define FER_LN_FWD8(C)                                                                                          \
+  hipLaunchKernelGGL(ln_fwd8_kernel<C>, g8, dim3(256), 0, (hipStream_t)stream, (const bf16*)x, (long)ldx, gamma, \
+                     beta, gamma_rows, row_div, (bf16*)y, (long)ldy, mean, rstd, M, D, eps);
+    switch ((D + 255) / 256) {
+      case 1: FER_LN_FWD8(1) break;
+      case 2: FER_LN_FWD8(2) break;
+      case 3: FER_LN_FWD8(3) break;
+      default: FER_LN_FWD8(4) break;
+    }
+#undef FER_LN_FWD8
+  } else if (dtype == FER_BF16)
     hipLaunchKernelGGL(ln_fwd_kernel<bf16>, grid, dim3(256), 0, (hipStream_t)stream, (const bf16*)x, (long)ldx, gamma,
                        beta, gamma_rows, row_div, (bf16*)y, (long)ldy, mean, rstd, M, D, eps);
   else
@@ -208,6 +412,25 @@ extern "C" int fer_layernorm_bwd(int dtype, const void* dy, int64_t lddy, const 
   const int nblk = ln_bwd_blocks(M);
   if (want && (!ws || ws_bytes < fer_layernorm_bwd_ws(M, D))) return set_error("layernorm_bwd: workspace too small");
   hipStream_t st = (hipStream_t)stream;
+  static const bool old_ln = getenv("FERVIT_LN_OLD") != nullptr;  // A/B switch
+  if (dtype == FER_BF16 && D % 8 == 0 && lddy % 8 == 0 && ldx % 8 == 0 && lddx % 8 == 0 && (!res || ldr % 8 == 0) &&
+      !old_ln) {
+#define FER_LN_BWD8(C)                                                                                          \
+  hipLaunchKernelGGL(ln_bwd8_kernel<C>, dim3(nblk), dim3(256), 0, st, (const bf16*)dy, (long)lddy, (const bf16*)x, \
+                     (long)ldx, mean, rstd, gamma, gamma_rows, row_div, (const bf16*)res, (long)ldr, (bf16*)dx,   \
+                     (long)lddx, (bf16*)dx_drop, drop_thresh, drop_scale, seed, ws, (int)want, M, D);
+    switch ((D + 255) / 256) {
+      case 1: FER_LN_BWD8(1) break;
+      case 2: FER_LN_BWD8(2) break;
+      case 3: FER_LN_BWD8(3) break;
+      default: FER_LN_BWD8(4) break;
+    }
+#undef FER_LN_BWD8
+    int rc = hip_check("layernorm_bwd8");
+    if (rc || !want) return rc;
+    part_reduce(ws, nblk, 3L * D, 3 * D, D, dgamma, dbeta, dbias, accumulate, nullptr, st);
+    return hip_check("layernorm_bwd_reduce");
+  }
 #define FER_LN_BWD(VP)                                                                                       \
   if (dtype == FER_BF16)                                                                                     \
     hipLaunchKernelGGL((ln_bwd_kernel<bf16, VP>), dim3(nblk), dim3(256), 0, st, (const bf16*)dy, (long)lddy,  \
