@@ -326,6 +326,8 @@ def main():
     ap.add_argument("--probe-steps", type=int, default=2, help="steps of the (untimed) roofline probe phase")
     ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
                     help="replay the whole step as a HIP graph (auto: on for the launch-bound small configs)")
+    ap.add_argument("--grad-dtype", choices=["fp32", "bf16"], default="fp32",
+                    help="N>1: dtype of the gradient all-reduce (bf16 halves the bytes; default fp32)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launch plumbing only (gloo, CPU): ranks rendezvous, barrier, rank 0 prints the JSON line")
     args = ap.parse_args()
@@ -375,7 +377,7 @@ def main():
     if world > 1:
         from fervit.ddp import DistributedDataParallel
 
-        net = DistributedDataParallel(model)
+        net = DistributedDataParallel(model, grad_dtype=torch.bfloat16 if args.grad_dtype == "bf16" else torch.float32)
     g = torch.Generator(device=device).manual_seed(42 + rank)
     x = torch.randn(B, *shape, device=device, generator=g)
     y = torch.randint(0, 7, (B,), device=device, generator=g)
@@ -457,7 +459,7 @@ def main():
             "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "bf16", "data": "synthetic (N(0,1) inputs, uniform labels), random init",
             "config": {"workload": desc, "per_gpu_batch": B, "global_batch": B * world, "tokens": N,
-                       "parallelism": f"dp{world}"},
+                       "parallelism": f"dp{world}", "grad_allreduce": args.grad_dtype if world > 1 else None},
             "step_ms_median": round(percentile(step_ms, 0.5), 3), "step_ms_p10": round(percentile(step_ms, 0.1), 3),
             "step_ms_p90": round(percentile(step_ms, 0.9), 3),
             "roofline": {"bound": "mfma", "kernel": "gemm_8ph_kernel (bf16 MFMA; every fwd + dgrad linear and the "

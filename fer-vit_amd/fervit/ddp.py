@@ -11,6 +11,12 @@ stream, overlapping communication with the remaining backward. A callback queued
 autograd engine makes the compute stream wait for every bucket before backward returns,
 so the optimizer always sees averaged gradients.
 
+`grad_dtype=torch.bfloat16` halves the bytes on the wire (ViT-B: 172 MB instead of 343 MB
+per step): each bucket is cast into a persistent bf16 communication buffer on the side stream
+(libfervit cast kernel), all-reduced in bf16, and cast back into the fp32 flat gradient before
+the optimizer. The sum is then rounded to bf16 at every reduction hop (like torch DDP's
+bf16 compression hook); the default stays fp32.
+
 Modules that are not fervit FerModules (e.g. CPU toy models in the gloo tests) get the
 same reducer fed by post-accumulate-grad hooks that copy p.grad into the flat buffer.
 """
@@ -38,7 +44,10 @@ class _Bucket:
 
 
 class Reducer:
-    def __init__(self, flat: FlatParams, params: List[nn.Parameter], group=None, bucket_cap_mb: float = 32.0):
+    def __init__(self, flat: FlatParams, params: List[nn.Parameter], group=None, bucket_cap_mb: float = 32.0,
+                 grad_dtype: torch.dtype = torch.float32):
+        if grad_dtype not in (torch.float32, torch.bfloat16):
+            raise ValueError("grad_dtype must be torch.float32 or torch.bfloat16")
         self.flat = flat
         self.group = group
         self.world = dist.get_world_size(group)
@@ -65,6 +74,8 @@ class Reducer:
         self.where: Dict[int, _Bucket] = {id(p): b for b in self.buckets for p in b.params}
         self.cuda = flat.grad.is_cuda
         self.side = torch.cuda.Stream(device=flat.grad.device) if self.cuda else None
+        self.comm = (torch.empty(flat.grad.numel(), dtype=torch.bfloat16, device=flat.grad.device)
+                     if grad_dtype == torch.bfloat16 else None)
         self.armed = False
         self.queued = False
 
@@ -102,9 +113,30 @@ class Reducer:
         if self.cuda:
             self.side.wait_stream(torch.cuda.current_stream(view.device))
             with torch.cuda.stream(self.side):
-                b.work = self._allreduce(view)
+                b.work = self._allreduce(self._to_wire(b, view))
         else:
-            b.work = self._allreduce(view)
+            b.work = self._allreduce(self._to_wire(b, view))
+
+    def _to_wire(self, b: _Bucket, view):
+        if self.comm is None:
+            return view
+        wire = self.comm[b.lo:b.hi]
+        if view.is_cuda:
+            from . import ops
+            ops.cast_bf16(view, out=wire)
+        else:  # CPU toy models of the gloo tests
+            wire.copy_(view)
+        return wire
+
+    def _from_wire(self, b: _Bucket):
+        if self.comm is None:
+            return
+        view, wire = self.flat.grad[b.lo:b.hi], self.comm[b.lo:b.hi]
+        if view.is_cuda:
+            from . import ops
+            ops.cast_f32(wire, out=view)
+        else:
+            view.copy_(wire)
 
     def _allreduce(self, view):
         if self.backend == "nccl":
@@ -125,6 +157,8 @@ class Reducer:
                 b.work.wait()
         if self.cuda:
             torch.cuda.current_stream(self.flat.grad.device).wait_stream(self.side)
+        for b in self.buckets:
+            self._from_wire(b)
         if self.backend != "nccl":
             for b in self.buckets:
                 self.flat.grad[b.lo:b.hi].div_(self.world)
@@ -135,7 +169,7 @@ class DistributedDataParallel(nn.Module):
     """Wrap a model; `forward` arms the reducer, backward all-reduces gradient buckets."""
 
     def __init__(self, module: nn.Module, bucket_cap_mb: float = 32.0, process_group=None,
-                 broadcast_params: bool = True):
+                 broadcast_params: bool = True, grad_dtype: torch.dtype = torch.float32):
         super().__init__()
         self.module = module
         self.group = process_group
@@ -153,7 +187,7 @@ class DistributedDataParallel(nn.Module):
         if broadcast_params:
             with torch.no_grad():
                 dist.broadcast(flat.data, src=0, group=process_group)
-        self.reducer = Reducer(flat, list(module.parameters()), process_group, bucket_cap_mb)
+        self.reducer = Reducer(flat, list(module.parameters()), process_group, bucket_cap_mb, grad_dtype)
         runtime.register_grad_ready_hook(self.reducer.on_ready)
 
     def _hook(self, p):

@@ -31,7 +31,7 @@ def _model():
     return m
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, wire):
     import sys
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -55,7 +55,7 @@ def _worker(rank, world, port, q):
         with torch.no_grad():
             for p in m.parameters():
                 p.add_(0.5)
-    ddp = DistributedDataParallel(m, bucket_cap_mb=0.05)
+    ddp = DistributedDataParallel(m, bucket_cap_mb=0.05, grad_dtype=getattr(torch, wire))
     xs, ys = x[rank * 4:(rank + 1) * 4], y[rank * 4:(rank + 1) * 4]
     crit(ddp(xs), ys).backward()
     err = max(((a.grad - b).norm() / (b.norm() + 1e-12)).item() for a, b in zip(m.parameters(), ref_g))
@@ -74,17 +74,19 @@ def _worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_ddp_device_gradients_and_replicas():
+@pytest.mark.parametrize("wire", ["float32", "bfloat16"])
+def test_ddp_device_gradients_and_replicas(wire):
+    """bfloat16: buckets cast by the libfervit kernels on the side stream, reduced in bf16."""
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, wire)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=150) for _ in range(world)]
     for p in procs:
         p.join(timeout=60)
     for rank, err, same in res:
-        assert err < 1e-5, (rank, err)
+        assert err < (1e-5 if wire == "float32" else 1e-2), (rank, err)
         assert same, rank
