@@ -112,6 +112,9 @@ class Reducer:
         view = self.flat.grad[b.lo:b.hi]
         if self.cuda:
             self.side.wait_stream(torch.cuda.current_stream(view.device))
+            wg = runtime.WGRAD.stream(view.device)  # weight gradients finish on their own stream
+            if wg is not None:
+                self.side.wait_stream(wg)
             with torch.cuda.stream(self.side):
                 b.work = self._allreduce(self._to_wire(b, view))
         else:

@@ -22,7 +22,7 @@ from typing import List, Optional, Sequence
 import torch
 
 from . import ops
-from .runtime import FlatParams, grads_ready, next_seed
+from .runtime import WGRAD, FlatParams, grads_ready, next_seed
 
 
 @dataclass
@@ -74,6 +74,11 @@ def _finish(flat: FlatParams, params, needs) -> None:
         flat.attach(p)
     if done:
         grads_ready(done)
+
+
+def _wgrad(dy, x, out, **kw):
+    """dW (+)= dy^T x on the weight-gradient stream (runtime.WGRAD)."""
+    return WGRAD.run(lambda: ops.linear_wgrad(dy, x, out, **kw), dy, x)
 
 
 def _empty(M, N, like, dtype=None):
@@ -135,11 +140,11 @@ class PostNormLayerFn(torch.autograd.Function):
                           dbeta=gn2b, dbias=gb2, accumulate=acc)
         dh2 = dz if dh2 is None else dh2
         if gw2 is not None:
-            ops.linear_wgrad(dh2, g, gw2, accumulate=acc)
+            _wgrad(dh2, g, gw2, accumulate=acc)
         # linear1.bias grad = column sums of dF, fused into this GEMM's epilogue
         dF = _dgrad(flat, dh2, w2, dt, aux=f, aux_act="mul", colsum=gb1, colsum_accumulate=acc)
         if gw1 is not None:
-            ops.linear_wgrad(dF, x1, gw1, accumulate=acc)
+            _wgrad(dF, x1, gw1, accumulate=acc)
         dx1 = _dgrad(flat, dF, w1, dt, res=dz)
         # LN1 (+ dropout of the attention branch, + out_proj bias grad)
         dy = torch.empty_like(y)
@@ -148,13 +153,13 @@ class PostNormLayerFn(torch.autograd.Function):
                           dbeta=gn1b, dbias=gout_b, accumulate=acc)
         dhh = dy if dhh is None else dhh
         if gout_w is not None:
-            ops.linear_wgrad(dhh, o, gout_w, accumulate=acc)
+            _wgrad(dhh, o, gout_w, accumulate=acc)
         do = _dgrad(flat, dhh, out_w, dt)
         dqkv = _empty(M, 3 * D, x)
         ops.attention_bwd(qkv, o, do, lse, dqkv, cfg.B, cfg.N, cfg.H, dh, dropout=pd, seed=seeds[0], colsum=gin_b,
                           colsum_accumulate=acc)
         if gin_w is not None:
-            ops.linear_wgrad(dqkv, x, gin_w, accumulate=acc)
+            _wgrad(dqkv, x, gin_w, accumulate=acc)
         dx = _dgrad(flat, dqkv, in_w, dt, res=dy)
         _finish(flat, P, needs)
         ctx.saved = None
@@ -206,21 +211,21 @@ class PreNormBlockFn(torch.autograd.Function):
         if gfc2_b is not None:
             ops.colsum(dout, gfc2_b, accumulate=acc)
         if gfc2_w is not None:
-            ops.linear_wgrad(dout, g, gfc2_w, accumulate=acc)
+            _wgrad(dout, g, gfc2_w, accumulate=acc)
         dF = _dgrad(flat, dout, fc2_w, dt, aux=f, aux_act="mul", colsum=gfc1_b, colsum_accumulate=acc)
         if gfc1_w is not None:
-            ops.linear_wgrad(dF, h2, gfc1_w, accumulate=acc)
+            _wgrad(dF, h2, gfc1_w, accumulate=acc)
         dh2 = _dgrad(flat, dF, fc1_w, dt)
         dx2 = ops.layernorm_bwd(dh2, x2, m2, r2, n2w.data, res=dout, dgamma=gn2w, dbeta=gn2b, accumulate=acc)
         if gproj_b is not None:
             ops.colsum(dx2, gproj_b, accumulate=acc)
         if gproj_w is not None:
-            ops.linear_wgrad(dx2, o, gproj_w, accumulate=acc)
+            _wgrad(dx2, o, gproj_w, accumulate=acc)
         do = _dgrad(flat, dx2, proj_w, dt)
         dqkv = _empty(M, 3 * D, x)
         ops.attention_bwd(qkv, o, do, lse, dqkv, cfg.B, cfg.N, cfg.H, dh, colsum=gqkv_b, colsum_accumulate=acc)
         if gqkv_w is not None:
-            ops.linear_wgrad(dqkv, h1, gqkv_w, accumulate=acc)
+            _wgrad(dqkv, h1, gqkv_w, accumulate=acc)
         dh1 = _dgrad(flat, dqkv, qkv_w, dt)
         dx = ops.layernorm_bwd(dh1, x, m1, r1, n1w.data, res=dx2, dgamma=gn1w, dbeta=gn1b, accumulate=acc)
         _finish(flat, P, needs)
@@ -262,12 +267,12 @@ class AdapterFn(torch.autograd.Function):
         if g2b is not None:
             ops.colsum(dout, g2b, accumulate=acc, scale=a)
         if g2w is not None:
-            ops.linear_wgrad(dout, v, g2w, accumulate=acc, post_scale=a)
+            _wgrad(dout, v, g2w, accumulate=acc, post_scale=a)
         du = _dgrad(flat, dout, fc2_w, dt, post_scale=a, aux=u, aux_act="mul")
         if g1b is not None:
             ops.colsum(du, g1b, accumulate=acc)
         if g1w is not None:
-            ops.linear_wgrad(du, x, g1w, accumulate=acc)
+            _wgrad(du, x, g1w, accumulate=acc)
         dx = _dgrad(flat, du, fc1_w, dt, res=dout)
         _finish(flat, P, needs)
         ctx.saved = None
@@ -308,7 +313,7 @@ class PatchTokensFn(torch.autograd.Function):
         if gb is not None:
             ops.colsum(demb, gb, accumulate=acc)
         if gw is not None:
-            ops.linear_wgrad(demb, cols, gw.view(D, -1), accumulate=acc)
+            _wgrad(demb, cols, gw.view(D, -1), accumulate=acc)
         _finish(flat, P, needs)
         ctx.saved = None
         return (None, None, None, None, None) + (None,) * len(P)
@@ -344,7 +349,7 @@ class LatentTokensFn(torch.autograd.Function):
         if gb is not None:
             ops.colsum(demb, gb, accumulate=acc)
         if gw is not None:
-            ops.linear_wgrad(demb, xc, gw, accumulate=acc)
+            _wgrad(demb, xc, gw, accumulate=acc)
         dx = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty(B * L, xc.shape[1], dtype=torch.float32, device=xc.device)

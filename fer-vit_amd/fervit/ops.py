@@ -44,13 +44,14 @@ def _dev(t: torch.Tensor) -> None:
 
 # ------------------------------------------------------------------ workspace
 class _Workspace:
-    """Grow-only fp32 scratch per device; all users are ordered on one stream."""
+    """Grow-only fp32 scratch per (device, slot, stream): users on one stream are ordered by it,
+    and the weight-gradient stream (runtime.WGRAD) gets buffers of its own."""
 
     def __init__(self):
         self.buf = {}
 
     def get(self, nbytes: int, device, slot: int = 0) -> torch.Tensor:
-        key = (device, slot)
+        key = (device, slot, torch.cuda.current_stream(device).cuda_stream)
         b = self.buf.get(key)
         n = max(1, (int(nbytes) + 3) // 4)
         if b is None or b.numel() < n:

@@ -11,7 +11,7 @@ from typing import Optional
 
 import torch
 
-from . import ops
+from . import ops, runtime
 from ._lib import AdamWSegment, check, lib
 
 
@@ -148,6 +148,7 @@ class FusedAdamW(torch.optim.Optimizer):
     def step(self, closure=None):
         loss = closure() if closure is not None else None
         flat = self._bind()
+        runtime.WGRAD.sync()  # weight gradients of the last backward (normally joined already)
         if self._frozen is not None:  # graph mode: static segments, device step counter
             dev, nseg, maxn = self._frozen
             half = flat.bf16()
@@ -193,6 +194,7 @@ def clip_grad_norm_(model, max_norm: float, sq_scale: float = 1.0, optimizer: Op
     (it starts zeroed and only gradient writes touch it), so they add nothing, like torch's
     skip of `p.grad is None`."""
     flat = model.fer_flat()
+    runtime.WGRAD.sync()
     out = torch.empty(2, dtype=torch.float32, device=flat.grad.device)
     ws = ops.WS.get(4 * 4096, flat.grad.device, slot=3)
     check(lib().fer_sumsq(flat.grad.data_ptr(), flat.numel, out.data_ptr(), ws.data_ptr(), ws.numel() * 4,

@@ -202,3 +202,61 @@ def grads_ready(params) -> None:
     """Layer backward finished writing these parameters' gradients."""
     for h in list(_HOOKS):
         h(params)
+
+
+# ------------------------------------------------------------ weight-gradient stream
+class _WgradStream:
+    """Weight gradients (dW = dY^T X) on a second HIP stream.
+
+    A layer's backward is a chain dY -> dX through dgrad GEMMs; the weight gradients hang off
+    that chain and nothing in the backward reads them. Issued on a side stream (after an event
+    on the compute stream), their split-K GEMMs take the CUs the dgrad GEMMs leave idle in their
+    last tile round (ViT-B: the N=768 GEMMs are 591 256x256 tiles = 2.31 rounds of 256 CUs).
+    Inputs are marked with record_stream so the caching allocator does not hand their memory
+    to the compute stream while the side stream reads it, and the first use in a backward
+    queues an autograd-engine callback that makes the compute stream wait for the side stream
+    before backward returns (optimizer, clipping and user code then see finished gradients).
+    Off under HIP-graph capture and with FERVIT_WGRAD_STREAM=0 (same stream as the dgrads)."""
+
+    def __init__(self):
+        self.streams = {}
+        self.join_queued = False
+        self.enabled = os.environ.get("FERVIT_WGRAD_STREAM", "1") != "0"
+
+    def stream(self, device):
+        return self.streams.get(device)
+
+    def run(self, fn, *inputs):
+        dev = inputs[0].device
+        if not self.enabled or torch.cuda.is_current_stream_capturing():
+            return fn()
+        main = torch.cuda.current_stream(dev)
+        side = self.streams.get(dev)
+        if side is None:
+            side = self.streams[dev] = torch.cuda.Stream(device=dev)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            out = fn()
+        for t in inputs:
+            t.record_stream(side)
+        if not self.join_queued:
+            try:
+                torch.autograd.Variable._execution_engine.queue_callback(self._join)
+                self.join_queued = True
+            except RuntimeError:  # not inside a backward pass: join right away
+                self._join()
+        return out
+
+    def _join(self):
+        self.join_queued = False
+        self.sync()
+
+    def sync(self):
+        """The current (compute) stream waits for every weight gradient issued so far."""
+        if not self.streams or torch.cuda.is_current_stream_capturing():
+            return
+        for dev, side in self.streams.items():
+            torch.cuda.current_stream(dev).wait_stream(side)
+
+
+WGRAD = _WgradStream()
