@@ -411,12 +411,17 @@ constexpr int fused_lds_bytes() {
 // lanes = columns (queries) and k = rows rbase + {0..3, 8..11} + 4*(lane>>5) (same k order as
 // rd_tr and the accumulator registers). Four consecutive 64-byte rows per 32-lane half: no
 // bank conflicts without a swizzle.
+// dS tile [32 keys][32 queries] bf16, 64-byte rows: 8-byte piece c of row r at piece c ^ ((r >> 1) & 7).
+// The writer's ds_write_b64 lane groups (16 consecutive rows, one piece) then cover 16 distinct bank
+// pairs (unswizzled: 8-way conflict, every row on banks {0,16} mod 32); the transposed reads (rows
+// R..R+3, all 8 pieces per 32-lane group) stay conflict-free.
+FER_DEV int ds_off(int r, int c8) { return r * 64 + ((c8 ^ ((r >> 1) & 7)) << 3); }
 FER_DEV bf16x8 rd_tr64(const char* img, int rbase, int lane) {
   const int gg = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
   const int R = rbase + 4 * (gg >> 1);
-  const int col = 16 * (gg & 1) + 4 * p;
-  const char* a1 = img + (R + q) * 64 + col * 2;
-  const char* a2 = img + (R + 8 + q) * 64 + col * 2;
+  const int c8 = 4 * (gg & 1) + p;
+  const char* a1 = img + ds_off(R + q, c8);
+  const char* a2 = img + ds_off(R + 8 + q, c8);
   short4_t t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4_t*)a1);
   short4_t t2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4_t*)a2);
   bf16x4 b1 = __builtin_bit_cast(bf16x4, t1), b2 = __builtin_bit_cast(bf16x4, t2);
@@ -540,7 +545,7 @@ __global__ __launch_bounds__(64 * NB) void attn_bwd_fused_bf16(const bf16* __res
     // dS tile -> LDS as [key][query] (bf16), read back below as the B operand of dQ^T
 #pragma unroll
     for (int g4 = 0; g4 < 4; ++g4)
-      *(bf16x4*)(Si + (lane & 31) * 64 + (8 * g4 + 4 * hh) * 2) =
+      *(bf16x4*)(Si + ds_off(lane & 31, 2 * g4 + hh)) =
           bf16x4{(bf16)st[4 * g4], (bf16)st[4 * g4 + 1], (bf16)st[4 * g4 + 2], (bf16)st[4 * g4 + 3]};
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
@@ -812,7 +817,7 @@ __global__ __launch_bounds__(64 * NB) void attn_bwd_pers(
         char* Si = Sall + w * 2048;
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4)
-          *(bf16x4*)(Si + (lane & 31) * 64 + (8 * g4 + 4 * hh) * 2) =
+          *(bf16x4*)(Si + ds_off(lane & 31, 2 * g4 + hh)) =
               bf16x4{(bf16)st[4 * g4], (bf16)st[4 * g4 + 1], (bf16)st[4 * g4 + 2], (bf16)st[4 * g4 + 3]};
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
