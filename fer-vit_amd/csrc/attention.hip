@@ -181,7 +181,7 @@ __global__ __launch_bounds__(64 * NB) __attribute__((amdgpu_waves_per_eu(4))) vo
     float bm = st[0];
 #pragma unroll
     for (int r = 1; r < 16; ++r) bm = fmaxf(bm, st[r]);
-    bm = fmaxf(bm, __shfl_xor(bm, 32, 64)) * sl2;
+    bm = xhalf_max(bm) * sl2;
     const float mn = fmaxf(m, bm);
     const float al = ex2(m - mn);
     m = mn;
@@ -201,7 +201,7 @@ __global__ __launch_bounds__(64 * NB) __attribute__((amdgpu_waves_per_eu(4))) vo
       for (int db = 0; db < 2; ++db) ot[db] = mfma32(rd_tr(Vi, kb * 32 + 16 * s2, db * 32, lane), pf, ot[db]);
     }
   }
-  l += __shfl_xor(l, 32, 64);
+  l = xhalf_sum(l);
   if (q < N) {
     store_rows_q(out + ((long)b * N + q) * ldo + h * dh, ot[0], ot[1], 1.f / l, hh, dh);
     if (hh == 0) lse[(long)bh * N + q] = (m + log2f(l)) * LN2;
@@ -334,7 +334,7 @@ __global__ __launch_bounds__(64 * (NB + 1)) void attn_fwd_pers(const bf16* __res
 #pragma unroll
         for (int r = 3; r < 15; r += 2) bm = fmaxf(fmaxf(bm, st[r]), st[r + 1]);
         bm = fmaxf(bm, st[15]);
-        bm = fmaxf(bm, __shfl_xor(bm, 32, 64)) * sl2;
+        bm = xhalf_max(bm) * sl2;
         if (__builtin_amdgcn_ballot_w64(bm > m + 8.f)) {  // wave-uniform
           const float mn = fmaxf(m, bm);
           const float al = ex2(m - mn);
@@ -374,7 +374,7 @@ __global__ __launch_bounds__(64 * (NB + 1)) void attn_fwd_pers(const bf16* __res
           for (int db = 0; db < 2; ++db) ot[db] = mfma32(vfr[s2][db], pf, ot[db]);
         }
       }
-      l += __shfl_xor(l, 32, 64);
+      l = xhalf_sum(l);
       if (q < N) {
         store_rows_q(out + ((long)b * N + q) * ldo + h * dh, ot[0], ot[1], dscale / l, hh, dh);
         if (hh == 0) lse[(long)bh * N + q] = (m + log2f(l)) * LN2;
@@ -612,8 +612,8 @@ __global__ __launch_bounds__(64 * NB) void attn_bwd_fused_bf16(const bf16* __res
         tk += dk[db][r];
         tv += dv[db][r];
       }
-      tk += __shfl_xor(tk, 32, 64);
-      tv += __shfl_xor(tv, 32, 64);
+      tk = xhalf_sum(tk);
+      tv = xhalf_sum(tv);
       if (hh == 0) {
         red[w * 192 + 64 + db * 32 + lane] = tk * scale;
         red[w * 192 + 128 + db * 32 + lane] = tv;
@@ -829,7 +829,7 @@ __global__ __launch_bounds__(64 * NB) void attn_bwd_pers(
           }
         }
         if (LAST && cs_part) {  // this wave's keys: sum over all queries of dS
-          cs += __shfl_xor(cs, 32, 64);
+          cs = xhalf_sum(cs);
           if (hh == 0) csl[w * 32 + lane] = cs;
         }
       }
@@ -913,8 +913,8 @@ __global__ __launch_bounds__(64 * NB) void attn_bwd_pers(
             tk += ok ? dk[db][r] : 0.f;
             tv += ok ? dv[db][r] : 0.f;
           }
-          tk += __shfl_xor(tk, 32, 64);
-          tv += __shfl_xor(tv, 32, 64);
+          tk = xhalf_sum(tk);
+          tv = xhalf_sum(tv);
           const int d = db * 32 + (lane & 31);
           float* o = cs_part + ((long)b * NB + w) * 3 * D + h * dh + d;
           if (hh == 0 && d < dh) {
@@ -1020,7 +1020,7 @@ __global__ __launch_bounds__(256) void attn_fwd_gen(const bf16* __restrict__ qkv
       float bm = st[0];
 #pragma unroll
       for (int r = 1; r < 16; ++r) bm = fmaxf(bm, st[r]);
-      bm = fmaxf(bm, __shfl_xor(bm, 32, 64)) * sl2;
+      bm = xhalf_max(bm) * sl2;
       const float mn = fmaxf(m, bm);
       const float al = ex2(m - mn);
       m = mn;
@@ -1044,7 +1044,7 @@ __global__ __launch_bounds__(256) void attn_fwd_gen(const bf16* __restrict__ qkv
       }
     }
   }
-  l += __shfl_xor(l, 32, 64);
+  l = xhalf_sum(l);
   if (qv) {
 #pragma unroll
     for (int hf = 0; hf < DH2; ++hf)
@@ -1084,7 +1084,7 @@ __global__ __launch_bounds__(256) void attn_dq_gen(const bf16* __restrict__ qkv,
 #pragma unroll
     for (int j = 0; j < 8; ++j) dsum += (float)ov[j] * (float)of[s][j];
   }
-  dsum += __shfl_xor(dsum, 32, 64);
+  dsum = xhalf_sum(dsum);
   const float lq = qv ? lse[(long)bh * N + q] * LOG2E : INFINITY;
   const uint32_t row = drop_row(bh, N, q);
   f32x16 dqt[2 * DH2];

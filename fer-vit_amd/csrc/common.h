@@ -216,6 +216,18 @@ FER_DEV void drop4(uint64_t seed, uint32_t idx, uint32_t thresh, float scale, f3
 }
 
 // ---------------------------------------------------------------- reductions
+// Combine a value with the other 32-lane half of the wave (lane l with l ^ 32) by
+// v_permlane32_swap: VALU only, no ds_bpermute round trip through the LDS pipe. The swap of v with
+// itself gives {own, partner} in lanes 0-31 and {partner, own} in 32-63; max / sum are symmetric,
+// so both halves get bit-identical results.
+FER_DEV float xhalf_max(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+FER_DEV float xhalf_sum(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
 FER_DEV float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

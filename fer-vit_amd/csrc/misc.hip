@@ -11,31 +11,34 @@ namespace fer {
 
 // ------------------------------------------------------------------ reductions
 // Deterministic second pass: out_k[c % seg] (+)= scale * sum_{b<nb} part[b*ld + c],
-// k = c / seg selects one of three outputs. 32 columns x 8 partial-row slices per block,
-// fixed summation order (slice-strided, then the 8 slices in order).
+// k = c / seg selects one of three outputs.
+// CB columns per block x (256 / CB) row phases, 8 independent accumulators per thread (8 loads in
+// flight; the partial slabs are read once and the sum is latency-bound otherwise). CB is picked so
+// that the grid covers the CUs (ViT-B: 2304 columns -> 288 blocks of 8 columns instead of 72 of
+// 32). Fixed association order for a given shape -> deterministic.
+template <int CB>
 __global__ __launch_bounds__(256) void part_reduce_kernel(const float* __restrict__ part, int nb, long ld, int ncols,
                                                           int seg, float* o0, float* o1, float* o2, int accumulate,
                                                           const float* __restrict__ scale) {
-  __shared__ float red[8][33];
-  const int cx = threadIdx.x & 31, j = threadIdx.x >> 5;
-  const int c = blockIdx.x * 32 + cx;
-  // 8 independent accumulators: 8 loads in flight per thread (the partial slabs are read once,
-  // the sum is latency-bound otherwise). Fixed association order -> deterministic.
+  constexpr int RP = 256 / CB;
+  __shared__ float red[RP][CB + 1];
+  const int cx = threadIdx.x % CB, j = threadIdx.x / CB;
+  const int c = blockIdx.x * CB + cx;
   float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if (c < ncols) {
     int b = j;
-    for (; b + 56 < nb; b += 64) {
+    for (; b + 7 * RP < nb; b += 8 * RP) {
 #pragma unroll
-      for (int u = 0; u < 8; ++u) s[u] += part[(long)(b + 8 * u) * ld + c];
+      for (int u = 0; u < 8; ++u) s[u] += part[(long)(b + RP * u) * ld + c];
     }
-    for (int u = 0; b < nb; b += 8, ++u) s[u] += part[(long)b * ld + c];
+    for (int u = 0; b < nb; b += RP, ++u) s[u] += part[(long)b * ld + c];
   }
   red[j][cx] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
   __syncthreads();
   if (j == 0 && c < ncols) {
     float t = 0.f;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) t += red[i][cx];
+#pragma unroll 8
+    for (int i = 0; i < RP; ++i) t += red[i][cx];
     if (scale) t *= *scale;
     const int k = c / seg, col = c - k * seg;
     float* o = k == 0 ? o0 : (k == 1 ? o1 : o2);
@@ -44,8 +47,12 @@ __global__ __launch_bounds__(256) void part_reduce_kernel(const float* __restric
 }
 void part_reduce(const float* part, int nb, long ld, int ncols, int seg, float* o0, float* o1, float* o2,
                  int accumulate, const float* scale, hipStream_t st) {
-  hipLaunchKernelGGL(part_reduce_kernel, dim3(ceil_div(ncols, 32)), dim3(256), 0, st, part, nb, ld, ncols, seg, o0, o1,
-                     o2, accumulate, scale);
+  if (ceil_div(ncols, 16) >= 256)
+    hipLaunchKernelGGL(part_reduce_kernel<16>, dim3(ceil_div(ncols, 16)), dim3(256), 0, st, part, nb, ld, ncols, seg,
+                       o0, o1, o2, accumulate, scale);
+  else
+    hipLaunchKernelGGL(part_reduce_kernel<8>, dim3(ceil_div(ncols, 8)), dim3(256), 0, st, part, nb, ld, ncols, seg,
+                       o0, o1, o2, accumulate, scale);
 }
 
 // ------------------------------------------------------------------ colsum
