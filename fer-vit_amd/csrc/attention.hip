@@ -275,33 +275,55 @@ __global__ __launch_bounds__(64 * (NB + 1)) void attn_fwd_pers(const bf16* __res
                                                                bf16* __restrict__ out, long ldo,
                                                                float* __restrict__ lse, uint32_t* __restrict__ mask,
                                                                int BH, int N, int H, int dh, float sl2, uint32_t thr,
-                                                               float dscale, uint64_t seed) {
+                                                               float dscale, uint64_t seed, WqArgs wq) {
   seed = step_seed(seed);
   constexpr int IMG = NB * 32 * 128;
-  __shared__ __attribute__((aligned(1024))) char lds[4 * IMG];  // 2 x (K image, V image)
+  __shared__ __attribute__((aligned(1024))) char lds[4 * IMG + 16];  // 2 x (K image, V image), unit hand-off
+  volatile int* hand = (volatile int*)(lds + 4 * IMG);
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), hh = lane >> 5;
   const u32x4 rs = rsrc4(qkv);
   const int q = w * 32 + (lane & 31);
-  int u = blockIdx.x;
+  // units: fixed stride, or the work queue `wq` (common.h): the first unit is blockIdx.x, the next
+  // one is claimed at the start, then the producer's lane 0 claims the unit after next while this
+  // one runs and hands it on through hand[k & 1] at the unit's last barrier
+  const bool claimer = threadIdx.x == 64 * NB;
+  int u, un;
+  if (wq.q) {
+    u = wq_first(BH);
+    if (u < 0) return;
+  } else {
+    u = blockIdx.x;
+    un = u + (int)gridDim.x < BH ? u + (int)gridDim.x : -1;
+  }
   bf16x8 qf[4];
   if (w == NB) {
     fwd_dma_unit<NB>(lds, rs, u, ldq, N, H, dh, lane);
+    int c0 = -1;
+    if (wq.q && claimer) c0 = wq_claim(wq.q, wq.base, BH);  // its round trip overlaps the DMA wait
     wait_vm<0>();
+    if (wq.q && claimer) hand[2] = c0;
   } else {
     fwd_load_q(qf, qkv, ldq, u, N, H, dh, q, hh);
   }
   bar_lds();
+  if (wq.q) un = __builtin_amdgcn_readfirstlane(hand[2]);
 #pragma unroll 1
   for (int k = 0;; ++k) {
-    const int un = u + gridDim.x;
     if (w == NB) {
-      if (un < BH) fwd_dma_unit<NB>(lds + ((k + 1) & 1) * 2 * IMG, rs, un, ldq, N, H, dh, lane);
+      int unn = -1;
+      if (wq.q) {
+        if (claimer && un >= 0) unn = wq_claim(wq.q, wq.base, BH);
+      } else if (un >= 0 && un + (int)gridDim.x < BH) {
+        unn = un + gridDim.x;
+      }
+      if (un >= 0) fwd_dma_unit<NB>(lds + ((k + 1) & 1) * 2 * IMG, rs, un, ldq, N, H, dh, lane);
       wait_vm<0>();
+      if (claimer) hand[k & 1] = unn;
     } else {
       const char* Ki = lds + (k & 1) * 2 * IMG;
       const char* Vi = Ki + IMG;
       bf16x8 qn[4];
-      if (un < BH) fwd_load_q(qn, qkv, ldq, un, N, H, dh, q, hh);
+      if (un >= 0) fwd_load_q(qn, qkv, ldq, un, N, H, dh, q, hh);
       const int bh = u, b = u / H, h = u - b * H;
       const uint32_t row = drop_row(bh, N, q);
       float m = -INFINITY, l = 0.f;
@@ -384,7 +406,8 @@ __global__ __launch_bounds__(64 * (NB + 1)) void attn_fwd_pers(const bf16* __res
     }
     bar_lds();  // the producer's DMA of unit un has landed (its wait_vm); every wave is done with unit u
     u = un;
-    if (u >= BH) break;
+    un = __builtin_amdgcn_readfirstlane(hand[k & 1]);
+    if (u < 0) break;
   }
 }
 
@@ -680,11 +703,13 @@ template <int NB>
 __global__ __launch_bounds__(64 * NB) void attn_bwd_pers(
     const bf16* __restrict__ qkv, long ldq, const bf16* __restrict__ out, long ldo, const bf16* __restrict__ dout,
     long lddo, const float* __restrict__ lse, const uint32_t* __restrict__ mask, bf16* __restrict__ dqkv, long lddq,
-    int BH, int N, int H, int dh, float scale, float sl2, float dscale, float* __restrict__ cs_part, int dbg) {
+    int BH, int N, int H, int dh, float scale, float sl2, float dscale, float* __restrict__ cs_part, int dbg,
+    WqArgs wq) {
   // dbg (FERVIT_ATTN_DBG, timing experiments only): 1 = no step math, 2 = no epilogue stores
   constexpr int IMG = NB * 32 * 128;
   constexpr int PREP = NB >= 4 ? 3 : NB - 1;  // step whose dQ phase computes the next unit's Dq
-  __shared__ __attribute__((aligned(1024))) char lds[pers_bwd_lds_bytes<NB>()];
+  __shared__ __attribute__((aligned(1024))) char lds[pers_bwd_lds_bytes<NB>() + 16];
+  volatile int* hand = (volatile int*)(lds + pers_bwd_lds_bytes<NB>());  // unit hand-off (work queue)
   char* Kimg = lds + 4 * IMG;               // NB x [32 keys][64 d] images
   char* Sall = lds + 5 * IMG;               // NB x [32 keys][32 queries] bf16 dS tiles
   float* lsd = (float*)(Sall + NB * 2048);  // 2 x {L[NB*32] = -lse/scale, Dq[NB*32]}
@@ -744,21 +769,37 @@ __global__ __launch_bounds__(64 * NB) void attn_bwd_pers(
     return mask ? mask[(((long)unit * NB + w) * NB + qb) * 32 + (lane & 31)] : 0xFFFFFFFFu;
   };
 
-  int u = blockIdx.x;
+  // units: fixed stride, or the work queue `wq` (common.h): the first unit is blockIdx.x, the next
+  // one is claimed at the start (overlapping the first unit's loads), then thread 0 claims the
+  // unit after next in each unit's epilogue and hands it on through hand[k & 1]
+  int u, un = -1;
+  if (wq.q) {
+    u = wq_first(BH);
+    if (u < 0) return;
+  } else {
+    u = blockIdx.x;
+    un = u + (int)gridDim.x < BH ? u + (int)gridDim.x : -1;
+  }
   bf16x8 kf[4], vf[4];
   prep_issue(u, 0);
   load_frag(kf, u, D);
   load_frag(vf, u, 2 * D);
   uint32_t mwn = mask_word(u, 0);
+  int c0 = -1;
+  if (wq.q && threadIdx.x == 0) c0 = wq_claim(wq.q, wq.base, BH);  // overlaps the loads' wait
   prep_finish(u, 0);
   write_kimg(kf);
   wait_vm<0>();
+  if (wq.q && threadIdx.x == 0) hand[2] = c0;
   bar_lds();
+  if (wq.q) un = __builtin_amdgcn_readfirstlane(hand[2]);
 
 #pragma unroll 1
   for (int k = 0;; ++k) {
-    const int cur = k & 1, un = u + gridDim.x;
-    const bool has_next = un < BH;
+    const int cur = k & 1;
+    const bool has_next = un >= 0;
+    int unn = -1;  // the unit after next (work queue: claimed by thread 0 in the epilogue below)
+    if (!wq.q && has_next && un + (int)gridDim.x < BH) unn = un + gridDim.x;
     const char* Qi = lds + cur * 2 * IMG;
     const char* Oi = Qi + IMG;
     const float* L = lsd + cur * 2 * NB * 32;
@@ -886,6 +927,8 @@ __global__ __launch_bounds__(64 * NB) void attn_bwd_pers(
     // ---- epilogue of unit u (one barrier)
     if (has_next) {
       if (PREP == NB - 1 && (dbg & 1)) prep_finish(un, cur ^ 1);
+      // the claim's round trip overlaps this wait for the next unit's rows
+      if (wq.q && threadIdx.x == 0) unn = wq_claim(wq.q, wq.base, BH);
       wait_vm<0>();  // this wave's DMA rows of the next unit, its K / V fragments, its mask word
     }
     if (!(dbg & 2)) {
@@ -946,8 +989,10 @@ __global__ __launch_bounds__(64 * NB) void attn_bwd_pers(
       write_kimg(kf);  // the last step's dQ phase (barrier above) was the last reader of the K images
       mwn = mw0;
     }
+    if (threadIdx.x == 0) hand[cur] = unn;
     bar_lds();  // next unit: K / Q / dO images (each wave waited for its DMA), L / Dq; staging read
     u = un;
+    un = __builtin_amdgcn_readfirstlane(hand[cur]);
     if (!has_next) break;
   }
 }
@@ -1387,6 +1432,11 @@ extern "C" int64_t fer_attention_ws(int dtype, int B, int N, int H) {
 
 static bool pers_path(int dtype, int N, int dh) { return dtype == FER_BF16 && N <= 224 && dh <= 64; }
 static int64_t lse_floats(int B, int N, int H) { return ((int64_t)B * H * N + 63) / 64 * 64; }
+// A/B switch: persistent kernels walk a fixed blockIdx stride instead of the work queue
+static bool fixed_stride() {
+  static const bool f = getenv("FERVIT_FIXED_STRIDE") != nullptr;
+  return f;
+}
 static int n_cus() {
   static const int n = [] {
     int dev = 0, c = 0;
@@ -1436,11 +1486,12 @@ extern "C" int fer_attention_fwd(int dtype, const void* qkv, int64_t ld_qkv, voi
     const int nb = (N + 31) / 32;
     uint32_t* mask = (drop_thresh && pers_path(dtype, N, dh)) ? (uint32_t*)(lse + lse_floats(B, N, H)) : nullptr;
     const int grid = std::min(B * H, n_cus());
+    const WqArgs wq = fixed_stride() ? WqArgs{} : wq_prepare_here(st, grid, B * H);
 #define FER_FPERS(NBV)                                                                                       \
   case NBV:                                                                                                  \
     hipLaunchKernelGGL(attn_fwd_pers<NBV>, dim3(grid), dim3(64 * (NBV + 1)), 0, st, (const bf16*)qkv,        \
                        (long)ld_qkv, (bf16*)out, (long)ld_out, lse, mask, B * H, N, H, dh, sl2, drop_thresh,  \
-                       drop_scale, seed);                                                                   \
+                       drop_scale, seed, wq);                                                               \
     break;
     switch (nb) {
       FER_FPERS(1) FER_FPERS(2) FER_FPERS(3) FER_FPERS(4) FER_FPERS(5) FER_FPERS(6) FER_FPERS(7)
@@ -1506,12 +1557,13 @@ extern "C" int fer_attention_bwd(int dtype, const void* qkv, int64_t ld_qkv, con
   if (pers_path(dtype, N, dh) && !general && !(old_bwd && !drop_thresh)) {
     const uint32_t* mask = drop_thresh ? (const uint32_t*)(lse + lse_floats(B, N, H)) : nullptr;
     const int grid = std::min(B * H, n_cus());
+    const WqArgs wq = fixed_stride() ? WqArgs{} : wq_prepare_here(st, grid, B * H);
 #define FER_PERS(NBV)                                                                                          \
   case NBV:                                                                                                    \
     hipLaunchKernelGGL(attn_bwd_pers<NBV>, dim3(grid), dim3(64 * NBV), 0, st, (const bf16*)qkv,                \
                        (long)ld_qkv, (const bf16*)out, (long)ld_out, (const bf16*)dout, (long)ld_dout, lse, mask, \
                        (bf16*)dqkv, (long)ld_dqkv, B * H, N, H, dh, scale, sl2, drop_scale, colsum ? ws : nullptr, \
-                       dbg);                                                                                     \
+                       dbg, wq);                                                                                 \
     break;
     switch (nb) {
       FER_PERS(1) FER_PERS(2) FER_PERS(3) FER_PERS(4) FER_PERS(5) FER_PERS(6) FER_PERS(7)

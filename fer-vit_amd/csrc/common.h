@@ -10,6 +10,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+#include <map>
+#include <mutex>
+
 #define FER_DEV __device__ __forceinline__
 
 typedef __bf16 bf16;
@@ -283,4 +287,73 @@ FER_DEV void dma4_asm(const void* lds, const u32x4& rs, uint32_t voff) {
 FER_DEV void bar_lds() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 FER_DEV __amdgpu_buffer_rsrc_t make_rsrc(const void* base) {
   return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)0x7FFFFFF0, 0x00020000);
+}
+
+// ---------------------------------------------------------------- dynamic work queues
+// Persistent kernels (one workgroup per CU) claim their work items from a device counter instead
+// of walking a fixed blockIdx stride. With a fixed stride, a workgroup whose CU is held by another
+// stream's kernel (RCCL's all-reduce during the DDP-overlapped backward, the weight-gradient
+// stream) only starts once some other workgroup of this kernel has EXITED, i.e. after all of its
+// items: the kernels ran 55-80 % longer with 16 of 256 CUs held (tools/hog_bench.py). Claiming
+// items dynamically, a late workgroup finds the queue drained.
+// Items are split into 8 classes (item & 7; blockIdx & 7 is the XCD a round-robin dispatch puts a
+// block on, so an XCD keeps walking its own L2-friendly share). Workgroup b's first item is b
+// itself (no claim at kernel start); the rest of class c is claimed from counter c, each on its own
+// 4 KB page. The counters are never reset: the host keeps each one's value at the start of the
+// launch (`base`, exact because every launch makes a known number of claims: one per dynamic
+// item plus one failing claim per workgroup that held an item), so a launch needs no exit
+// counter and no reset. Slots are per code object and per stream; under stream capture (the
+// replayed graph could not keep the bases current) the kernels walk the fixed stride.
+constexpr int FER_WQ_SLOTS = 32;
+constexpr int FER_WQ_PAD = 1024;
+static __device__ int fer_wq[FER_WQ_SLOTS][8 * FER_WQ_PAD];
+
+struct WqArgs {
+  int* q;  // null: fixed stride
+  uint32_t base[8];
+};
+
+// First item of this workgroup (-1: none).
+FER_DEV int wq_first(int n) { return (int)blockIdx.x < n ? (int)blockIdx.x : -1; }
+// Next item of this workgroup's class; -1 when drained (then claim no more).
+FER_DEV int wq_claim(int* q, const uint32_t* base, int n) {
+  const int cls = blockIdx.x & 7;
+  const uint32_t t =
+      (uint32_t)__hip_atomic_fetch_add(q + cls * FER_WQ_PAD, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) -
+      base[cls];
+  const int nwg = ((int)gridDim.x - cls + 7) >> 3, items = (n - cls + 7) >> 3;
+  return (long)t < (long)items - nwg ? cls + 8 * (nwg + (int)t) : -1;
+}
+// Host: the queue of this code object for a launch of `grid` workgroups over `n` items on `st`
+// (q = null: fixed stride). Advances the slot's bases by the claims the launch will make.
+static inline WqArgs wq_prepare_here(hipStream_t st, int grid, int n) {
+  struct Slot {
+    int* dev;
+    uint32_t base[8];
+  };
+  static std::mutex mu;
+  static std::map<hipStream_t, Slot> slots;
+  static int* pool = nullptr;
+  WqArgs a{};
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return a;
+  std::lock_guard<std::mutex> lk(mu);
+  if (!pool && hipGetSymbolAddress((void**)&pool, HIP_SYMBOL(fer_wq)) != hipSuccess) {
+    pool = nullptr;
+    return a;
+  }
+  auto it = slots.find(st);
+  if (it == slots.end()) {
+    if ((int)slots.size() >= FER_WQ_SLOTS) return a;  // more streams than slots: fixed stride
+    Slot sl{pool + 8 * FER_WQ_PAD * (int)slots.size(), {}};
+    it = slots.emplace(st, sl).first;
+  }
+  Slot& sl = it->second;
+  a.q = sl.dev;
+  for (int c = 0; c < 8; ++c) {
+    a.base[c] = sl.base[c];
+    const int nwg = std::max(0, (grid - c + 7) / 8), items = std::max(0, (n - c + 7) / 8);
+    sl.base[c] += (uint32_t)(std::max(0, items - nwg) + std::min(nwg, items));
+  }
+  return a;
 }

@@ -843,8 +843,11 @@ FER_DEV unsigned long long stamp_now() {
 #define FER_STAMP(i) do {} while (0)
 #endif
 
+// claim_slot (work-queue mode): thread 0 claims a tile at the start of this one, before the
+// prologue's operand DMA, and parks the id in that LDS word after the prologue's wait (which
+// retires the atomic together with the previous tile's epilogue stores and the first K-tile)
 template <bool AKC, bool BKC, int MT>
-FER_DEV void tile_8ph(const GemmArgs& g, const EpiArgs& e, int bid, char* smem) {
+FER_DEV void tile_8ph(const GemmArgs& g, const EpiArgs& e, int bid, char* smem, volatile int* claim_slot) {
   typedef typename Acc<MT>::T AccT;
   constexpr int UNIT = 16384, BUF = 4 * UNIT;  // A0 A1 B0 B1
   constexpr int FM = 128 / MT, FN = 64 / MT;   // MFMA blocks per wave (rows, cols)
@@ -895,6 +898,8 @@ FER_DEV void tile_8ph(const GemmArgs& g, const EpiArgs& e, int bid, char* smem) 
     for (int j = 0; j < FM; ++j) acc[i][j] = AccT{};
   bf16x8 fa[2][KS][QJ], fb[2][KS][QI];
 
+  int claimed = -1;
+  if (claim_slot && tid == 0) claimed = wq_claim(g.tq, g.tq_base, g.tiles_m * g.tiles_n);
   if (nk > 0) {
     iA0(0); iB0(0); iA1(0); iB1(0);
     if (nk > 1) {
@@ -907,6 +912,7 @@ FER_DEV void tile_8ph(const GemmArgs& g, const EpiArgs& e, int bid, char* smem) 
     if (wr) __builtin_amdgcn_s_barrier();  // stagger: waves 4-7 one barrier behind
     asm volatile("" ::: "memory");
   }
+  if (claim_slot && tid == 0) *claim_slot = claimed;
   FER_STAMP(1);
 
   for (int T = 0; T < nk; ++T) {
@@ -982,14 +988,30 @@ FER_DEV void tile_8ph(const GemmArgs& g, const EpiArgs& e, int bid, char* smem) 
 // is kept since grid % 8 == 0). A workgroup goes from one tile's epilogue stores straight into
 // the next tile's operand DMA, so the store drain overlaps the next tile's first loads instead
 // of sitting between a workgroup's exit and its successor's launch.
-template <bool AKC, bool BKC, int MT>
+// DYN: tiles from the per-stream work queue (common.h wq_*; the class of tile bid is bid & 7, the
+// XCD tile_of's remap gives it): the first tile is blockIdx.x, each tile claims the next one at
+// its start (tile_8ph claim_slot) and hands it on through LDS at its end. !DYN: fixed stride
+// (split-K launches, stream capture, FERVIT_FIXED_STRIDE).
+template <bool AKC, bool BKC, int MT, bool DYN>
 __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmArgs g, EpiArgs e) {
-  __shared__ __attribute__((aligned(1024))) char smem[8 * 16384];
+  __shared__ __attribute__((aligned(1024))) char smem[8 * 16384 + 16];
   const int ntiles = g.tiles_m * g.tiles_n;
+  if constexpr (!DYN) {
 #pragma unroll 1
-  for (int bid = blockIdx.x; bid < ntiles; bid += gridDim.x) {
-    tile_8ph<AKC, BKC, MT>(g, e, bid, smem);
-    __syncthreads();  // every wave is done with the epilogue's LDS before the next tile's DMA
+    for (int bid = blockIdx.x; bid < ntiles; bid += gridDim.x) {
+      tile_8ph<AKC, BKC, MT>(g, e, bid, smem, nullptr);
+      __syncthreads();  // every wave is done with the epilogue's LDS before the next tile's DMA
+    }
+  } else {
+    volatile int* slot = (volatile int*)(smem + 8 * 16384);
+    int bid = wq_first(ntiles), par = 0;
+#pragma unroll 1
+    while (bid >= 0) {
+      tile_8ph<AKC, BKC, MT>(g, e, bid, smem, slot + par);
+      __syncthreads();  // every wave is done with the epilogue's LDS before the next tile's DMA
+      bid = __builtin_amdgcn_readfirstlane(slot[par]);
+      par ^= 1;
+    }
   }
 }
 
@@ -1084,8 +1106,18 @@ static int launch_8ph(GemmArgs g, const EpiArgs& e, hipStream_t st) {
   static const bool persist = getenv("FERVIT_GEMM_NOPERSIST") == nullptr;  // A/B switch
   const int ntiles = g.tiles_m * g.tiles_n;
   const int gx = persist ? std::min(ntiles, std::max(8, ncu / 8 * 8)) : ntiles;
+  static const bool fixed = getenv("FERVIT_FIXED_STRIDE") != nullptr;  // A/B switch
+  g.tq = nullptr;
+  if (persist && !fixed && g.splits == 1) {
+    const WqArgs w = wq_prepare_here(st, gx, ntiles);
+    g.tq = w.q;
+    for (int c = 0; c < 8; ++c) g.tq_base[c] = w.base[c];
+  }
   dim3 grid(gx, g.splits);
-  hipLaunchKernelGGL((gemm_8ph_kernel<AKC, BKC, MT>), grid, dim3(512), 0, st, g, e);
+  if (g.tq)
+    hipLaunchKernelGGL((gemm_8ph_kernel<AKC, BKC, MT, true>), grid, dim3(512), 0, st, g, e);
+  else
+    hipLaunchKernelGGL((gemm_8ph_kernel<AKC, BKC, MT, false>), grid, dim3(512), 0, st, g, e);
   return 0;
 }
 

@@ -349,3 +349,55 @@ def test_transposed_bf16_shadow():
     assert torch.equal(t, ps[1].data.to(torch.bfloat16).t().contiguous())
     with pytest.raises(ValueError):
         flat.half_t_view(ps[3])
+
+
+def test_persistent_work_queue_streams_and_capture():
+    """The persistent GEMM / attention kernels claim tiles from per-stream device counters whose
+    launch-start values the host tracks (common.h wq_*): many back-to-back launches on one stream,
+    launches alternating with a second stream that runs concurrently, and a graph-captured launch
+    (fixed stride under capture) replayed between eager ones must all give the first launch's bits."""
+    o = ops()
+    g = torch.Generator(device=DEV).manual_seed(3)
+    M, N, K = 256 * 70, 1024, 192  # 280 tiles of 256x256: 8-phase persistent kernel
+    x = torch.randn(M, K, device=DEV, generator=g).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV, generator=g) / math.sqrt(K)).to(torch.bfloat16)
+    ref = o.linear_fwd(x, w)
+    assert rel_err(ref, x.float() @ w.float().t()) < 1e-2
+    B, Nt, H, dh = 48, 197, 12, 64  # 576 (batch, head) units
+    qkv = torch.randn(B * Nt, 3 * H * dh, device=DEV, generator=g).to(torch.bfloat16)
+    dout = torch.randn(B * Nt, H * dh, device=DEV, generator=g).to(torch.bfloat16)
+    sv = o.attention_saved(qkv, B, Nt, H, dh, dropout=0.1)
+    ao = torch.empty(B * Nt, H * dh, device=DEV, dtype=torch.bfloat16)
+    dq = torch.empty_like(qkv)
+    o.attention_fwd(qkv, ao, sv, B, Nt, H, dh, dropout=0.1, seed=4)
+    o.attention_bwd(qkv, ao, dout, sv, dq, B, Nt, H, dh, dropout=0.1, seed=4)
+    ao_ref, dq_ref = ao.clone(), dq.clone()
+    side = torch.cuda.Stream()
+    outs = []
+    for i in range(40):
+        st = side if i % 3 == 1 else torch.cuda.current_stream()
+        with torch.cuda.stream(st):
+            outs.append(o.linear_fwd(x, w))
+    torch.cuda.synchronize()
+    for y in outs:
+        assert torch.equal(y, ref)
+    for _ in range(6):
+        o.attention_fwd(qkv, ao, sv, B, Nt, H, dh, dropout=0.1, seed=4)
+        o.attention_bwd(qkv, ao, dout, sv, dq, B, Nt, H, dh, dropout=0.1, seed=4)
+        assert torch.equal(ao, ao_ref) and torch.equal(dq, dq_ref)
+    # captured launch (fixed stride) between eager launches on the capture stream's queue
+    cap_out = torch.empty_like(ref)
+    gr = torch.cuda.CUDAGraph()
+    s2 = torch.cuda.Stream()
+    s2.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s2):
+        o.linear_fwd(x, w, out=cap_out)
+        with torch.cuda.graph(gr, stream=s2):
+            o.linear_fwd(x, w, out=cap_out)
+    torch.cuda.current_stream().wait_stream(s2)
+    for _ in range(3):
+        cap_out.zero_()
+        gr.replay()
+        assert torch.equal(o.linear_fwd(x, w), ref)
+        torch.cuda.synchronize()
+        assert torch.equal(cap_out, ref)
