@@ -16,7 +16,8 @@ that time); one HIP event per step boundary gives the per-step median / p10 / p9
 roofline: the dominant kernel is `gemm_8ph_kernel`, the bf16 MFMA GEMM of every forward and
 input-gradient linear (QKV, out-proj, fc1, fc2, patch embed; ~55 % of the step). Its launches
 are timed in a separate PROBE phase after the timed region (HIP events on the launch stream
-around each launch, so the timed region carries no probe events): achieved = sum over one
+around each launch, so the timed region carries no probe events; weight gradients on the compute
+stream during the probe, so no launch shares the chip with a concurrent one): achieved = sum over one
 step's 8-phase launches of 2*M*N*K / sum of their durations, vs the dense bf16 MFMA peak
 (MI355X_MICROARCH.md: 256 CU x 4 SIMD x 1024 FLOP/clk x 2.4 GHz = 2516.6 TFLOP/s).
 `traffic` = HBM bytes per launch of that kernel from rocprofv3 PMC passes (FETCH_SIZE,
@@ -368,7 +369,7 @@ def main():
             rccl = "unknown"
 
     import fervit
-    from fervit import ops
+    from fervit import ops, runtime
 
     fervit.manual_seed(1234 + rank)
     torch.manual_seed(42)
@@ -438,11 +439,17 @@ def main():
     # probe phase (untimed): HIP events around every gemm_8ph launch of a few eager steps
     if use_graph:
         graph.release()
+    # the weight-gradient stream is switched off for the probe: with it, a dgrad launch shares the
+    # chip with a concurrent split-K wgrad and its events would time that contention (and the wait
+    # for CUs the wgrad holds), not the kernel
+    wg_on = runtime.WGRAD.enabled
+    runtime.WGRAD.enabled = False
     probe.on = True
     for _ in range(args.probe_steps):
         step()
     torch.cuda.synchronize()
     probe.on = False
+    runtime.WGRAD.enabled = wg_on
     ps = probe.summary(args.probe_steps)
     ms = el / args.steps * 1e3
     imgs = world * B * args.steps / el
