@@ -128,6 +128,77 @@ FER_DEV void epi8_bf16(const EpiArgs& e, long m, long n, f32x4& v0, f32x4& v1, f
   }
 }
 
+// Epilogue kinds with the flags fixed at compile time (the 8-phase kernel's hot shapes): the
+// generic epi8_bf16 tests every flag per row piece, and its branches and the register shuffles
+// between them cost more issue slots than the arithmetic of the plain and residual epilogues.
+// Same operations in the same order as epi8_bf16, so the results are bit-identical.
+enum { EPI_GEN = 0, EPI_STORE = 1, EPI_GATE = 2, EPI_RES = 3, EPI_MUL = 4 };
+//   EPI_STORE: c = alpha*acc + bias                                   (qkv fwd, out-proj dgrad)
+//   EPI_GATE : c = drop(gelu(v)), pre = drop(gelu'(v)), v = alpha*acc + bias      (fc1 fwd)
+//   EPI_RES  : c = drop(alpha*acc + bias) + res                (out-proj / fc2 fwd, dgrad + res)
+//   EPI_MUL  : c = (alpha*acc + bias) * aux                      (fc2 dgrad through the gate)
+// (bf16 c without accumulate, no post_scale; dropout is a run-time choice in GATE and RES)
+template <int S>
+FER_DEV void epi8_t(const EpiArgs& e, long m, long n, f32x4& v0, f32x4& v1, f32x4 b0, f32x4 b1, bf16x8 x,
+                    float ps, uint64_t seed) {
+  if constexpr (S == EPI_GEN) {
+    epi8_bf16(e, m, n, v0, v1, b0, b1, x, ps, seed);
+  } else {
+    v0 = v0 * e.alpha + b0;
+    v1 = v1 * e.alpha + b1;
+    if constexpr (S == EPI_GATE) {
+      f32x4 g0, g1;
+      f32x2 t;
+      v0.xy = gelu_and_grad2(v0.xy, t); g0.xy = t;
+      v0.zw = gelu_and_grad2(v0.zw, t); g0.zw = t;
+      v1.xy = gelu_and_grad2(v1.xy, t); g1.xy = t;
+      v1.zw = gelu_and_grad2(v1.zw, t); g1.zw = t;
+      if (e.drop_thresh) {
+        const uint32_t idx = (uint32_t)m * (uint32_t)e.drop_ld + (uint32_t)n;
+        const uint32_t k = keep4(seed, idx, e.drop_thresh) | (keep4(seed, idx + 4, e.drop_thresh) << 4);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          v0[r] = (k >> r) & 1 ? v0[r] * e.drop_scale : 0.f;
+          v1[r] = (k >> (4 + r)) & 1 ? v1[r] * e.drop_scale : 0.f;
+          g0[r] = (k >> r) & 1 ? g0[r] * e.drop_scale : 0.f;
+          g1[r] = (k >> (4 + r)) & 1 ? g1[r] * e.drop_scale : 0.f;
+        }
+      }
+      *(bf16x8*)((bf16*)e.pre + m * e.ldp + n) = pack8(g0, g1);
+    }
+    if constexpr (S == EPI_RES) {
+      if (e.drop_thresh) {
+        const uint32_t idx = (uint32_t)m * (uint32_t)e.drop_ld + (uint32_t)n;
+        const uint32_t k = keep4(seed, idx, e.drop_thresh) | (keep4(seed, idx + 4, e.drop_thresh) << 4);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          v0[r] = (k >> r) & 1 ? v0[r] * e.drop_scale : 0.f;
+          v1[r] = (k >> (4 + r)) & 1 ? v1[r] * e.drop_scale : 0.f;
+        }
+      }
+      v0 += lo4(x);
+      v1 += hi4(x);
+    }
+    if constexpr (S == EPI_MUL) {
+      v0 *= lo4(x);
+      v1 *= hi4(x);
+    }
+    *(bf16x8*)((bf16*)e.c + m * e.ldc + n) = pack8(v0, v1);
+  }
+}
+
+// kind for a launch (EPI_GEN unless every flag matches one of the fixed kinds)
+static inline int epi_kind(const EpiArgs& e) {
+  if (e.c_f32 || e.accumulate || e.post_scale) return EPI_GEN;
+  const int act = e.act & 15;
+  const bool gate = (e.act & FER_PRE_GATE) && e.pre;
+  if (gate) return (act == FER_ACT_GELU && !e.aux && !e.res) ? EPI_GATE : EPI_GEN;
+  if (e.pre || act) return EPI_GEN;
+  if (e.aux) return (e.aux_act == FER_ACT_MUL && !e.res && !e.drop_thresh) ? EPI_MUL : EPI_GEN;
+  if (e.res) return EPI_RES;
+  return e.drop_thresh ? EPI_GEN : EPI_STORE;
+}
+
 template <typename T>
 FER_DEV void epi4(const EpiArgs& e, long m, long n, f32x4 v, uint64_t seed) {
   const int act = e.act & 15;
@@ -297,15 +368,37 @@ FER_DEV typename Acc<MT>::T mfma(bf16x8 a, bf16x8 b, typename Acc<MT>::T c) {
   else return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
+#ifdef FER_GEMM_STAMPS
+// diagnostic build only: s_memtime at the epilogue's stage boundaries (lane 0 of waves 0 and 4 of
+// workgroup 0; the last tile's values remain)
+__device__ unsigned long long g_epst[2][16];
+#define EP_STAMP(i)                                                          \
+  do {                                                                       \
+    if (ep_on) {                                                             \
+      unsigned long long t_;                                                 \
+      __builtin_amdgcn_sched_barrier(0);                                     \
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
+      __builtin_amdgcn_sched_barrier(0);                                     \
+      if (lane == 0) g_epst[(tid_ >> 6) >> 2][i] = t_;                       \
+    }                                                                        \
+  } while (0)
+#else
+#define EP_STAMP(i) do {} while (0)
+#endif
+
 // ---- epilogue. Accumulator element (i, j, q, r) -> tile row/col. Split-K partials go to
 // the fp32 slab; otherwise each wave-row half of the tile (in EPC row chunks) is staged
 // through LDS as fp32 with padded rows and every thread applies the epilogue on 4 consecutive
 // columns of one row: all global traffic of the epilogue is row-contiguous.
-template <int BM, int BN, int WM, int WN, int MT, int EPC, int SMEMB, typename AccT, int FN, int FM>
+template <int BM, int BN, int WM, int WN, int MT, int EPC, int SMEMB, int EK = EPI_GEN, typename AccT, int FN, int FM>
 FER_DEV void tile_epilogue(const GemmArgs& g, const EpiArgs& e, AccT (&acc)[FN][FM], char* smem, int m0, int n0,
                            int ks, int wm, int wn, int lane) {
   int tid_ = threadIdx.x;  // laundered: not hoisted out of a persistent tile loop
   asm volatile("" : "+v"(tid_));
+#ifdef FER_GEMM_STAMPS
+  const bool ep_on = blockIdx.x == 0 && ks == 0 && ((tid_ >> 6) & 3) == 0;
+#endif
+  EP_STAMP(0);
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int NQ = MT == 32 ? 4 : 1;
   const int lr = MT == 32 ? (lane & 31) : (lane & 15);
@@ -414,19 +507,32 @@ FER_DEV void tile_epilogue(const GemmArgs& g, const EpiArgs& e, AccT (&acc)[FN][
     __syncthreads();  // staging and X[h&1] (all waves' DMA) visible
   };
   f32x4 cs0 = f32x4{0.f, 0.f, 0.f, 0.f}, cs1 = cs0;  // fused column sums of this thread's rows
+  // software-pipelined over the thread's rows: the LDS reads of row it+1 are issued before row it's
+  // math and stores, so their latency hides behind it (one row at a time exposed it every row)
   auto finish = [&](int h) {
     const char* xh = xb + (h & 1) * XBYTES;
+    f32x4 v0 = *(const f32x4*)(stg + swz(tr, tc)), v1 = *(const f32x4*)(stg + swz(tr, tc + 4));
+    bf16x8 x = xs ? *(const bf16x8*)(xh + (tr * BN + tc) * 2) : bf16x8{};
 #pragma unroll 1
     for (int it = 0; it < IT; ++it) {
       const int r = tr + it * RPI;
       const long m = m0 + h * EROWS + r;
-      f32x4 v0 = *(const f32x4*)(stg + swz(r, tc)), v1 = *(const f32x4*)(stg + swz(r, tc + 4));
-      const bf16x8 x = xs ? *(const bf16x8*)(xh + (r * BN + tc) * 2) : bf16x8{};
+      f32x4 n0 = v0, n1 = v1;
+      bf16x8 nx = x;
+      if (it + 1 < IT) {
+        const int rn = r + RPI;
+        n0 = *(const f32x4*)(stg + swz(rn, tc));
+        n1 = *(const f32x4*)(stg + swz(rn, tc + 4));
+        if (xs) nx = *(const bf16x8*)(xh + (rn * BN + tc) * 2);
+      }
       if (nok && m < g.M) {
-        epi8_bf16(e, m, n, v0, v1, b0, b1, x, ps, seed);
+        epi8_t<EK>(e, m, n, v0, v1, b0, b1, x, ps, seed);
         cs0 += v0;
         cs1 += v1;
       }
+      v0 = n0;
+      v1 = n1;
+      x = nx;
     }
   };
   if (xs) issue_x(0);
@@ -434,9 +540,13 @@ FER_DEV void tile_epilogue(const GemmArgs& g, const EpiArgs& e, AccT (&acc)[FN][
   for (int p = 0; p < EPC; ++p) {
     const int h0 = 2 * p, h1 = 2 * p + 1;
     stage(h0, h0 / EPC, 0);
+    EP_STAMP(1 + 4 * p);
     finish(h0);
+    EP_STAMP(2 + 4 * p);
     stage(h1, h1 / EPC, EPC == 2 ? 1 : 0);
+    EP_STAMP(3 + 4 * p);
     finish(h1);
+    EP_STAMP(4 + 4 * p);
   }
   if (g.cs_part) {  // column partial sums of this tile -> cs_part[tile row][n], fixed order
     __syncthreads();  // staging area free
@@ -846,7 +956,7 @@ FER_DEV unsigned long long stamp_now() {
 // claim_slot (work-queue mode): thread 0 claims a tile at the start of this one, before the
 // prologue's operand DMA, and parks the id in that LDS word after the prologue's wait (which
 // retires the atomic together with the previous tile's epilogue stores and the first K-tile)
-template <bool AKC, bool BKC, int MT>
+template <bool AKC, bool BKC, int MT, int EK>
 FER_DEV void tile_8ph(const GemmArgs& g, const EpiArgs& e, int bid, char* smem, volatile int* claim_slot) {
   typedef typename Acc<MT>::T AccT;
   constexpr int UNIT = 16384, BUF = 4 * UNIT;  // A0 A1 B0 B1
@@ -974,7 +1084,7 @@ FER_DEV void tile_8ph(const GemmArgs& g, const EpiArgs& e, int bid, char* smem, 
     return;
   }
   static_assert(64 * (256 + 4) * 4 <= 2 * BUF, "epilogue staging (2 chunks per half) must fit");
-  tile_epilogue<256, 256, 2, 4, MT, 2, 2 * BUF>(g, e, acc, smem, m0, n0, ks, wr, wc, lane);
+  tile_epilogue<256, 256, 2, 4, MT, 2, 2 * BUF, EK>(g, e, acc, smem, m0, n0, ks, wr, wc, lane);
   FER_STAMP(3);
 #ifdef FER_GEMM_STAMPS
   if (st_on) {
@@ -992,14 +1102,14 @@ FER_DEV void tile_8ph(const GemmArgs& g, const EpiArgs& e, int bid, char* smem, 
 // XCD tile_of's remap gives it): the first tile is blockIdx.x, each tile claims the next one at
 // its start (tile_8ph claim_slot) and hands it on through LDS at its end. !DYN: fixed stride
 // (split-K launches, stream capture, FERVIT_FIXED_STRIDE).
-template <bool AKC, bool BKC, int MT, bool DYN>
+template <bool AKC, bool BKC, int MT, bool DYN, int EK>
 __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmArgs g, EpiArgs e) {
   __shared__ __attribute__((aligned(1024))) char smem[8 * 16384 + 16];
   const int ntiles = g.tiles_m * g.tiles_n;
   if constexpr (!DYN) {
 #pragma unroll 1
     for (int bid = blockIdx.x; bid < ntiles; bid += gridDim.x) {
-      tile_8ph<AKC, BKC, MT>(g, e, bid, smem, nullptr);
+      tile_8ph<AKC, BKC, MT, EK>(g, e, bid, smem, nullptr);
       __syncthreads();  // every wave is done with the epilogue's LDS before the next tile's DMA
     }
   } else {
@@ -1007,7 +1117,7 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmArgs g, EpiArgs e)
     int bid = wq_first(ntiles), par = 0;
 #pragma unroll 1
     while (bid >= 0) {
-      tile_8ph<AKC, BKC, MT>(g, e, bid, smem, slot + par);
+      tile_8ph<AKC, BKC, MT, EK>(g, e, bid, smem, slot + par);
       __syncthreads();  // every wave is done with the epilogue's LDS before the next tile's DMA
       bid = __builtin_amdgcn_readfirstlane(slot[par]);
       par ^= 1;
@@ -1114,16 +1224,39 @@ static int launch_8ph(GemmArgs g, const EpiArgs& e, hipStream_t st) {
     for (int c = 0; c < 8; ++c) g.tq_base[c] = w.base[c];
   }
   dim3 grid(gx, g.splits);
-  if (g.tq)
-    hipLaunchKernelGGL((gemm_8ph_kernel<AKC, BKC, MT, true>), grid, dim3(512), 0, st, g, e);
-  else
-    hipLaunchKernelGGL((gemm_8ph_kernel<AKC, BKC, MT, false>), grid, dim3(512), 0, st, g, e);
+  // fixed-flag epilogues for the K-contiguous MT16 kernel (the forward and transposed-shadow dgrad
+  // path); FERVIT_EPI_GENERIC=1 keeps the generic one (A/B switch)
+  static const bool gen_only = getenv("FERVIT_EPI_GENERIC") != nullptr;
+  const int ek = (AKC && BKC && MT == 16 && !g.partial && !gen_only) ? epi_kind(e) : EPI_GEN;
+#define FER_8PH(DY, K) hipLaunchKernelGGL((gemm_8ph_kernel<AKC, BKC, MT, DY, K>), grid, dim3(512), 0, st, g, e)
+#define FER_8PH_K(DY)                                  \
+  if constexpr (AKC && BKC && MT == 16) {              \
+    switch (ek) {                                      \
+      case EPI_STORE: FER_8PH(DY, EPI_STORE); break;   \
+      case EPI_GATE: FER_8PH(DY, EPI_GATE); break;     \
+      case EPI_RES: FER_8PH(DY, EPI_RES); break;       \
+      case EPI_MUL: FER_8PH(DY, EPI_MUL); break;       \
+      default: FER_8PH(DY, EPI_GEN); break;            \
+    }                                                  \
+  } else {                                             \
+    FER_8PH(DY, EPI_GEN);                              \
+  }
+  if (g.tq) {
+    FER_8PH_K(true)
+  } else {
+    FER_8PH_K(false)
+  }
+#undef FER_8PH_K
+#undef FER_8PH
   return 0;
 }
 
 #ifdef FER_GEMM_STAMPS
 extern "C" int fer_debug_gemm_stamps(unsigned long long* host, int n) {
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * n) == hipSuccess ? 0 : 1;
+}
+extern "C" int fer_debug_gemm_ep_stamps(unsigned long long* host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_epst), sizeof(unsigned long long) * 32) == hipSuccess ? 0 : 1;
 }
 #endif
 

@@ -29,6 +29,10 @@ def main():
         fn = lambda: ops.linear_fwd(x, w1)
     elif case == "fc1fused":
         fn = lambda: ops.linear_fwd(x, w1, b1, pre=pre, act="gelu", dropout=0.1, seed=7)
+    elif case == "fc1gate":
+        fn = lambda: ops.linear_fwd(x, w1, b1, pre=pre, pre_gate=True, act="gelu", dropout=0.1, seed=7)
+    elif case == "fc2res":  # fc2 fwd with bias + dropout + residual (K = 3072)
+        fn = lambda: ops.linear_fwd(h, w2, b1[:D], res=x, dropout=0.1, seed=7)
     else:  # fc2: K = 3072
         fn = lambda: ops.linear_fwd(h, w2)
     for _ in range(3):
@@ -39,11 +43,19 @@ def main():
     buf = (ctypes.c_ulonglong * n)()
     L.fer_debug_gemm_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
     assert L.fer_debug_gemm_stamps(ctypes.addressof(buf), n) == 0
+    ep = (ctypes.c_ulonglong * 32)()
+    L.fer_debug_gemm_ep_stamps.argtypes = [ctypes.c_void_p]
+    assert L.fer_debug_gemm_ep_stamps(ctypes.addressof(ep)) == 0
+    names = ["stage0", "finish0", "stage1", "finish1", "stage2", "finish2", "stage3", "finish3"]
+    for w in range(2):
+        e = ep[w * 16:(w + 1) * 16]
+        print(f"epilogue wave {4 * w} (last tile of WG 0): total {e[8] - e[0]} cyc: " +
+              "  ".join(f"{nm} {e[i + 1] - e[i]}" for i, nm in enumerate(names)))
     for w in range(2):
         s = buf[w * 260:(w + 1) * 260]
         t0 = s[0]
         print(f"wave {4 * w}: prologue {s[1] - s[0]} cyc, main loop {s[2] - s[1]}, epilogue {s[3] - s[2]}")
-        nk = 12 if case != "fc2" else 16
+        nk = 16 if case.startswith("fc2") else 12
         tot = [0, 0, 0, 0]
         cnt = 0
         for T in range(nk):
