@@ -25,6 +25,8 @@
 // fp32 path (parity mode): a plain LDS-tiled VALU kernel with the same epilogue.
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "common.h"
 #include "fervit_internal.h"
 
@@ -132,15 +134,32 @@ FER_DEV void epi8_bf16(const EpiArgs& e, long m, long n, f32x4& v0, f32x4& v1, f
 // generic epi8_bf16 tests every flag per row piece, and its branches and the register shuffles
 // between them cost more issue slots than the arithmetic of the plain and residual epilogues.
 // Same operations in the same order as epi8_bf16, so the results are bit-identical.
-enum { EPI_GEN = 0, EPI_STORE = 1, EPI_GATE = 2, EPI_RES = 3, EPI_MUL = 4 };
+enum { EPI_GEN = 0, EPI_STORE = 1, EPI_GATE = 2, EPI_RES = 3, EPI_MUL = 4, EPI_RES2 = 5, EPI_MUL2 = 6 };
 //   EPI_STORE: c = alpha*acc + bias                                   (qkv fwd, out-proj dgrad)
 //   EPI_GATE : c = drop(gelu(v)), pre = drop(gelu'(v)), v = alpha*acc + bias      (fc1 fwd)
 //   EPI_RES  : c = drop(alpha*acc + bias) + res                (out-proj / fc2 fwd, dgrad + res)
 //   EPI_MUL  : c = (alpha*acc + bias) * aux                      (fc2 dgrad through the gate)
 // (bf16 c without accumulate, no post_scale; dropout is a run-time choice in GATE and RES)
-template <int S>
+// EPI_RES2 / EPI_MUL2: the same arithmetic as RES / MUL; the tile epilogue loads the row operand
+// straight into registers instead of LDS, which frees the LDS for two staging areas.
+constexpr int epi_base(int S) { return S == EPI_RES2 ? EPI_RES : (S == EPI_MUL2 ? EPI_MUL : S); }
+// Keep bits of 8 consecutive elements from an even index (4 hashes), as compares: the same
+// decisions as keep4 (u16 >= thr; the high half as h >= thr << 16) without packing them into an
+// integer and testing its bits again per element.
+FER_DEV void keep8(uint64_t seed, uint32_t idx, uint32_t thr, bool (&kp)[8]) {
+  const uint32_t thr_hi = thr << 16;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint32_t h = fer_hash(seed, (idx >> 1) + q);
+    kp[2 * q] = (h & 0xFFFFu) >= thr;
+    kp[2 * q + 1] = h >= thr_hi;
+  }
+}
+
+template <int S0>
 FER_DEV void epi8_t(const EpiArgs& e, long m, long n, f32x4& v0, f32x4& v1, f32x4 b0, f32x4 b1, bf16x8 x,
                     float ps, uint64_t seed) {
+  constexpr int S = epi_base(S0);
   if constexpr (S == EPI_GEN) {
     epi8_bf16(e, m, n, v0, v1, b0, b1, x, ps, seed);
   } else {
@@ -154,26 +173,26 @@ FER_DEV void epi8_t(const EpiArgs& e, long m, long n, f32x4& v0, f32x4& v1, f32x
       v1.xy = gelu_and_grad2(v1.xy, t); g1.xy = t;
       v1.zw = gelu_and_grad2(v1.zw, t); g1.zw = t;
       if (e.drop_thresh) {
-        const uint32_t idx = (uint32_t)m * (uint32_t)e.drop_ld + (uint32_t)n;
-        const uint32_t k = keep4(seed, idx, e.drop_thresh) | (keep4(seed, idx + 4, e.drop_thresh) << 4);
+        bool kp[8];
+        keep8(seed, (uint32_t)m * (uint32_t)e.drop_ld + (uint32_t)n, e.drop_thresh, kp);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          v0[r] = (k >> r) & 1 ? v0[r] * e.drop_scale : 0.f;
-          v1[r] = (k >> (4 + r)) & 1 ? v1[r] * e.drop_scale : 0.f;
-          g0[r] = (k >> r) & 1 ? g0[r] * e.drop_scale : 0.f;
-          g1[r] = (k >> (4 + r)) & 1 ? g1[r] * e.drop_scale : 0.f;
+          v0[r] = kp[r] ? v0[r] * e.drop_scale : 0.f;
+          v1[r] = kp[4 + r] ? v1[r] * e.drop_scale : 0.f;
+          g0[r] = kp[r] ? g0[r] * e.drop_scale : 0.f;
+          g1[r] = kp[4 + r] ? g1[r] * e.drop_scale : 0.f;
         }
       }
       *(bf16x8*)((bf16*)e.pre + m * e.ldp + n) = pack8(g0, g1);
     }
     if constexpr (S == EPI_RES) {
       if (e.drop_thresh) {
-        const uint32_t idx = (uint32_t)m * (uint32_t)e.drop_ld + (uint32_t)n;
-        const uint32_t k = keep4(seed, idx, e.drop_thresh) | (keep4(seed, idx + 4, e.drop_thresh) << 4);
+        bool kp[8];
+        keep8(seed, (uint32_t)m * (uint32_t)e.drop_ld + (uint32_t)n, e.drop_thresh, kp);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          v0[r] = (k >> r) & 1 ? v0[r] * e.drop_scale : 0.f;
-          v1[r] = (k >> (4 + r)) & 1 ? v1[r] * e.drop_scale : 0.f;
+          v0[r] = kp[r] ? v0[r] * e.drop_scale : 0.f;
+          v1[r] = kp[4 + r] ? v1[r] * e.drop_scale : 0.f;
         }
       }
       v0 += lo4(x);
@@ -194,8 +213,9 @@ static inline int epi_kind(const EpiArgs& e) {
   const bool gate = (e.act & FER_PRE_GATE) && e.pre;
   if (gate) return (act == FER_ACT_GELU && !e.aux && !e.res) ? EPI_GATE : EPI_GEN;
   if (e.pre || act) return EPI_GEN;
-  if (e.aux) return (e.aux_act == FER_ACT_MUL && !e.res && !e.drop_thresh) ? EPI_MUL : EPI_GEN;
-  if (e.res) return EPI_RES;
+  static const bool xdma = getenv("FERVIT_EPI_XDMA") != nullptr;  // A/B: row operand through LDS-DMA
+  if (e.aux) return (e.aux_act == FER_ACT_MUL && !e.res && !e.drop_thresh) ? (xdma ? EPI_MUL : EPI_MUL2) : EPI_GEN;
+  if (e.res) return xdma ? EPI_RES : EPI_RES2;
   return e.drop_thresh ? EPI_GEN : EPI_STORE;
 }
 
@@ -509,7 +529,7 @@ FER_DEV void tile_epilogue(const GemmArgs& g, const EpiArgs& e, AccT (&acc)[FN][
   f32x4 cs0 = f32x4{0.f, 0.f, 0.f, 0.f}, cs1 = cs0;  // fused column sums of this thread's rows
   // software-pipelined over the thread's rows: the LDS reads of row it+1 are issued before row it's
   // math and stores, so their latency hides behind it (one row at a time exposed it every row)
-  auto finish = [&](int h) {
+  auto finish = [&](int h, const char* stg) {
     const char* xh = xb + (h & 1) * XBYTES;
     f32x4 v0 = *(const f32x4*)(stg + swz(tr, tc)), v1 = *(const f32x4*)(stg + swz(tr, tc + 4));
     bf16x8 x = xs ? *(const bf16x8*)(xh + (tr * BN + tc) * 2) : bf16x8{};
@@ -535,18 +555,116 @@ FER_DEV void tile_epilogue(const GemmArgs& g, const EpiArgs& e, AccT (&acc)[FN][
       x = nx;
     }
   };
-  if (xs) issue_x(0);
+  if constexpr ((EK == EPI_RES2 || EK == EPI_MUL2) && EPC == 2 && 2 * EROWS * SROW <= SMEMB) {
+    // row operand in registers: this thread's 2 x IT rows of a round are loaded before the round's
+    // staging (round 0's at entry, round 1's once round 0's accumulators are in LDS), so they fly
+    // during the staging and the other round; loads issued before the stores retire first (vmcnt)
+    const bf16* xg = (const bf16*)xs;
+    auto load_x = [&](int p, bf16x8 (&xr)[2 * IT]) {
+#pragma unroll
+      for (int k = 0; k < 2 * IT; ++k) {
+        const long m = m0 + ((k / IT) * EPC + p) * EROWS + tr + (k % IT) * RPI;
+        xr[k] = (nok && m < g.M) ? *(const bf16x8*)(xg + m * ldxs + n) : bf16x8{};
+      }
+    };
+    auto finish_x = [&](int h, const char* stg, const bf16x8* xr) {
+      f32x4 v0 = *(const f32x4*)(stg + swz(tr, tc)), v1 = *(const f32x4*)(stg + swz(tr, tc + 4));
+#pragma unroll
+      for (int it = 0; it < IT; ++it) {
+        const int r = tr + it * RPI;
+        const long m = m0 + h * EROWS + r;
+        f32x4 n0 = v0, n1 = v1;
+        if (it + 1 < IT) {
+          n0 = *(const f32x4*)(stg + swz(r + RPI, tc));
+          n1 = *(const f32x4*)(stg + swz(r + RPI, tc + 4));
+        }
+        if (nok && m < g.M) {
+          epi8_t<EK>(e, m, n, v0, v1, b0, b1, xr[it], ps, seed);
+          cs0 += v0;
+          cs1 += v1;
+        }
+        v0 = n0;
+        v1 = n1;
+      }
+    };
+    auto put = [&](auto sub) {
+#pragma unroll
+      for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int jj = 0; jj < FJ; ++jj)
+#pragma unroll
+          for (int q = 0; q < NQ; ++q) {
+            const int j = decltype(sub)::value * FJ + jj;
+            *(f32x4*)(stg + wm * (EROWS * SROW) + swz(jj * MT + lr, wn * TN + i * MT + 8 * q + lc)) =
+                f32x4{acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]};
+          }
+    };
+    bf16x8 xr[2 * IT];
+    load_x(0, xr);
+    __syncthreads();
+    put(std::integral_constant<int, 0>{});
+    __syncthreads();
+    EP_STAMP(1);
+    finish_x(0, stg, xr);
+    EP_STAMP(2);
+    finish_x(EPC, stg + EROWS * SROW, xr + IT);
+    EP_STAMP(3);
+    load_x(1, xr);
+    __syncthreads();
+    put(std::integral_constant<int, 1>{});
+    __syncthreads();
+    EP_STAMP(5);
+    finish_x(1, stg, xr);
+    EP_STAMP(6);
+    finish_x(EPC + 1, stg + EROWS * SROW, xr + IT);
+    EP_STAMP(7);
+    EP_STAMP(4);
+    EP_STAMP(8);
+  } else if constexpr ((EK == EPI_STORE || EK == EPI_GATE) && EPC == 2 && 2 * EROWS * SROW <= SMEMB) {
+    // no row operand: the X buffers' LDS holds a second staging area, so both wave-row halves
+    // stage a chunk at once (all waves write, two barrier rounds instead of four); chunk sub p of
+    // half w is tile chunk h = 2w + p (rows 64h..64h+63)
 #pragma unroll 1
-  for (int p = 0; p < EPC; ++p) {
-    const int h0 = 2 * p, h1 = 2 * p + 1;
-    stage(h0, h0 / EPC, 0);
-    EP_STAMP(1 + 4 * p);
-    finish(h0);
-    EP_STAMP(2 + 4 * p);
-    stage(h1, h1 / EPC, EPC == 2 ? 1 : 0);
-    EP_STAMP(3 + 4 * p);
-    finish(h1);
-    EP_STAMP(4 + 4 * p);
+    for (int p = 0; p < EPC; ++p) {
+      __syncthreads();  // every wave is done with both staging areas
+      // accumulator indices must be compile-time constants (a run-time p would index the
+      // accumulator array dynamically: scratch)
+      auto put = [&](auto sub) {
+#pragma unroll
+        for (int i = 0; i < FN; ++i)
+#pragma unroll
+          for (int jj = 0; jj < FJ; ++jj)
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+              const int j = decltype(sub)::value * FJ + jj;
+              *(f32x4*)(stg + wm * (EROWS * SROW) + swz(jj * MT + lr, wn * TN + i * MT + 8 * q + lc)) =
+                  f32x4{acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]};
+            }
+      };
+      if (p == 0) put(std::integral_constant<int, 0>{});
+      else put(std::integral_constant<int, 1>{});
+      __syncthreads();
+      EP_STAMP(1 + 4 * p);
+      finish(p, stg);
+      EP_STAMP(2 + 4 * p);
+      finish(EPC + p, stg + EROWS * SROW);
+      EP_STAMP(3 + 4 * p);
+      EP_STAMP(4 + 4 * p);
+    }
+  } else {
+    if (xs) issue_x(0);
+#pragma unroll 1
+    for (int p = 0; p < EPC; ++p) {
+      const int h0 = 2 * p, h1 = 2 * p + 1;
+      stage(h0, h0 / EPC, 0);
+      EP_STAMP(1 + 4 * p);
+      finish(h0, stg);
+      EP_STAMP(2 + 4 * p);
+      stage(h1, h1 / EPC, EPC == 2 ? 1 : 0);
+      EP_STAMP(3 + 4 * p);
+      finish(h1, stg);
+      EP_STAMP(4 + 4 * p);
+    }
   }
   if (g.cs_part) {  // column partial sums of this tile -> cs_part[tile row][n], fixed order
     __syncthreads();  // staging area free
@@ -1236,6 +1354,8 @@ static int launch_8ph(GemmArgs g, const EpiArgs& e, hipStream_t st) {
       case EPI_GATE: FER_8PH(DY, EPI_GATE); break;     \
       case EPI_RES: FER_8PH(DY, EPI_RES); break;       \
       case EPI_MUL: FER_8PH(DY, EPI_MUL); break;       \
+      case EPI_RES2: FER_8PH(DY, EPI_RES2); break;     \
+      case EPI_MUL2: FER_8PH(DY, EPI_MUL2); break;     \
       default: FER_8PH(DY, EPI_GEN); break;            \
     }                                                  \
   } else {                                             \
