@@ -359,6 +359,9 @@ def main():
         traffic, traffic_detail = pmc_traffic()
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
+    prio = os.environ.get("FERVIT_STEP_PRIO")
+    if prio is not None:  # A/B: run the step on a stream of this priority (the weight-gradient stream keeps 0)
+        torch.cuda.set_stream(torch.cuda.Stream(device=device, priority=int(prio)))
     rccl = None
     if world > 1:
         dist.init_process_group("nccl", device_id=device)
