@@ -157,6 +157,44 @@ FER_DEV f32x2 gelu_and_grad2(f32x2 x, f32x2& grad) {
   grad = __builtin_elementwise_fma(x * 0.39894228040143268f, e, cdf);
   return x * cdf;
 }
+// Four independent pairs stage by stage (the same per-element operations as gelu_and_grad2): a
+// dependent packed-f32 op right after its producer costs a hazard s_nop, and one pair's
+// polynomial is a chain of them; interleaving the pairs fills those slots.
+FER_DEV void gelu_and_grad8(f32x2 (&x)[4], f32x2 (&grad)[4]) {
+  f32x2 e[4], z[4], t[4], y[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const f32x2 h = -0.5f * x[i] * x[i];
+    e[i] = f32x2{__expf(h[0]), __expf(h[1])};
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) z[i] = x[i] * 0.70710678118654752f;
+  const f32x2 ka = kpk(0.3275911f);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const f32x2 d = __builtin_elementwise_fma(ka, __builtin_elementwise_abs(z[i]), f32x2(1.0f));
+    t[i] = f32x2{__builtin_amdgcn_rcpf(d[0]), __builtin_amdgcn_rcpf(d[1])};
+  }
+  const f32x2 k0 = kpk(1.061405429f), k1 = kpk(-1.453152027f);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) y[i] = __builtin_elementwise_fma(k0, t[i], k1);
+  const f32x2 k2 = kpk(1.421413741f);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) y[i] = __builtin_elementwise_fma(y[i], t[i], k2);
+  const f32x2 k3 = kpk(-0.284496736f);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) y[i] = __builtin_elementwise_fma(y[i], t[i], k3);
+  const f32x2 k4 = kpk(0.254829592f);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) y[i] = __builtin_elementwise_fma(y[i], t[i], k4);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const f32x2 r = 1.0f - y[i] * t[i] * e[i];
+    const f32x2 cdf = 0.5f * (1.0f + __builtin_elementwise_copysign(r, z[i]));
+    grad[i] = __builtin_elementwise_fma(x[i] * 0.39894228040143268f, e[i], cdf);
+    x[i] = x[i] * cdf;
+  }
+}
 FER_DEV float act_fwd(int act, float x) {
   return act == FER_ACT_GELU ? gelu_erf(x) : (act == FER_ACT_RELU ? fmaxf(x, 0.f) : x);
 }

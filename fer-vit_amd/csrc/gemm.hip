@@ -168,10 +168,11 @@ FER_DEV void epi8_t(const EpiArgs& e, long m, long n, f32x4& v0, f32x4& v1, f32x
     if constexpr (S == EPI_GATE) {
       f32x4 g0, g1;
       f32x2 t;
-      v0.xy = gelu_and_grad2(v0.xy, t); g0.xy = t;
-      v0.zw = gelu_and_grad2(v0.zw, t); g0.zw = t;
-      v1.xy = gelu_and_grad2(v1.xy, t); g1.xy = t;
-      v1.zw = gelu_and_grad2(v1.zw, t); g1.zw = t;
+      f32x2 xs[4] = {v0.xy, v0.zw, v1.xy, v1.zw}, gs[4];
+      gelu_and_grad8(xs, gs);
+      v0.xy = xs[0]; v0.zw = xs[1]; v1.xy = xs[2]; v1.zw = xs[3];
+      g0.xy = gs[0]; g0.zw = gs[1]; g1.xy = gs[2]; g1.zw = gs[3];
+      (void)t;
       if (e.drop_thresh) {
         bool kp[8];
         keep8(seed, (uint32_t)m * (uint32_t)e.drop_ld + (uint32_t)n, e.drop_thresh, kp);
@@ -527,32 +528,19 @@ FER_DEV void tile_epilogue(const GemmArgs& g, const EpiArgs& e, AccT (&acc)[FN][
     __syncthreads();  // staging and X[h&1] (all waves' DMA) visible
   };
   f32x4 cs0 = f32x4{0.f, 0.f, 0.f, 0.f}, cs1 = cs0;  // fused column sums of this thread's rows
-  // software-pipelined over the thread's rows: the LDS reads of row it+1 are issued before row it's
-  // math and stores, so their latency hides behind it (one row at a time exposed it every row)
   auto finish = [&](int h, const char* stg) {
     const char* xh = xb + (h & 1) * XBYTES;
-    f32x4 v0 = *(const f32x4*)(stg + swz(tr, tc)), v1 = *(const f32x4*)(stg + swz(tr, tc + 4));
-    bf16x8 x = xs ? *(const bf16x8*)(xh + (tr * BN + tc) * 2) : bf16x8{};
 #pragma unroll 1
     for (int it = 0; it < IT; ++it) {
       const int r = tr + it * RPI;
       const long m = m0 + h * EROWS + r;
-      f32x4 n0 = v0, n1 = v1;
-      bf16x8 nx = x;
-      if (it + 1 < IT) {
-        const int rn = r + RPI;
-        n0 = *(const f32x4*)(stg + swz(rn, tc));
-        n1 = *(const f32x4*)(stg + swz(rn, tc + 4));
-        if (xs) nx = *(const bf16x8*)(xh + (rn * BN + tc) * 2);
-      }
+      f32x4 v0 = *(const f32x4*)(stg + swz(r, tc)), v1 = *(const f32x4*)(stg + swz(r, tc + 4));
+      const bf16x8 x = xs ? *(const bf16x8*)(xh + (r * BN + tc) * 2) : bf16x8{};
       if (nok && m < g.M) {
         epi8_t<EK>(e, m, n, v0, v1, b0, b1, x, ps, seed);
         cs0 += v0;
         cs1 += v1;
       }
-      v0 = n0;
-      v1 = n1;
-      x = nx;
     }
   };
   if constexpr ((EK == EPI_RES2 || EK == EPI_MUL2) && EPC == 2 && 2 * EROWS * SROW <= SMEMB) {
