@@ -451,6 +451,46 @@ FER_DEV bf16x8 rd_tr64(const char* img, int rbase, int lane) {
   return bf16x8{b1[0], b1[1], b1[2], b1[3], b2[0], b2[1], b2[2], b2[3]};
 }
 
+// Lane offsets of the LDS reads above, computed once per step instead of per read. The swizzles
+// depend on row bits 1-3 only, so a read at row base R (a multiple of 16) is the R = 0 offset + the
+// row term; rd_tr's second 32-column half (cb = 32) flips chunk bit 2 of a chunk index below 4,
+// i.e. byte bit 6 (XOR 64); rd_row's chunk 2s + hh is the s = 0 chunk XOR 2s (byte XOR 32s).
+struct TrB {
+  int a1, a2;  // rd_tr(img, 0, 0) byte offsets of the two row groups (cb = 32: XOR 64)
+};
+FER_DEV TrB tr_base(int lane) {
+  const int gg = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int R = 4 * (gg >> 1);
+  const int c = (16 * (gg & 1) + 4 * p) >> 3, half = (p & 1) * 8;
+  const int r1 = R + q, r2 = R + 8 + q;
+  TrB b;
+  b.a1 = r1 * 128 + ((c ^ swz(r1)) << 4) + half;
+  b.a2 = r2 * 128 + ((c ^ swz(r2)) << 4) + half;
+  return b;
+}
+// == rd_tr(img, R, 32 * hi, lane) for img + R * 128 passed as `img`
+FER_DEV bf16x8 rd_trb(const char* img, const TrB& b, bool hi) {
+  short4_t t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4_t*)(img + (hi ? (b.a1 ^ 64) : b.a1)));
+  short4_t t2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4_t*)(img + (hi ? (b.a2 ^ 64) : b.a2)));
+  bf16x4 b1 = __builtin_bit_cast(bf16x4, t1), b2 = __builtin_bit_cast(bf16x4, t2);
+  return bf16x8{b1[0], b1[1], b1[2], b1[3], b2[0], b2[1], b2[2], b2[3]};
+}
+// == rd_row(img, R + (lane & 31), 2s + (lane >> 5)) for img + R * 128 passed as `img`
+FER_DEV int row_base(int lane) { return (lane & 31) * 128 + (((lane >> 5) ^ swz(lane & 31)) << 4); }
+FER_DEV bf16x8 rd_rowb(const char* img, int rb, int s) { return *(const bf16x8*)(img + (rb ^ (s << 5))); }
+// == rd_tr64(img, R, lane) for img + R * 64 passed as `img`
+FER_DEV int2 tr64_base(int lane) {
+  const int gg = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int R = 4 * (gg >> 1), c8 = 4 * (gg & 1) + p;
+  return int2{ds_off(R + q, c8), ds_off(R + 8 + q, c8)};
+}
+FER_DEV bf16x8 rd_tr64b(const char* img, int2 b) {
+  short4_t t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4_t*)(img + b.x));
+  short4_t t2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4_t*)(img + b.y));
+  bf16x4 b1 = __builtin_bit_cast(bf16x4, t1), b2 = __builtin_bit_cast(bf16x4, t2);
+  return bf16x8{b1[0], b1[1], b1[2], b1[3], b2[0], b2[1], b2[2], b2[3]};
+}
+
 // dQacc: [NB*32 queries][64 d] fp32, 16-byte chunk index XOR (row & 15)
 FER_DEV int dq_off(int row, int chunk) { return row * 256 + ((chunk ^ (row & 15)) << 4); }
 
@@ -820,6 +860,10 @@ __global__ __launch_bounds__(64 * NB) void attn_bwd_pers(
         if (i == 0 && has_next) prep_issue(un, cur ^ 1);
         int qb = w + i;
         if (qb >= NB) qb -= NB;
+        const TrB tb = tr_base(lane);
+        const int rb = row_base(lane);
+        const char* Qq = Qi + qb * 4096;
+        const char* Oq = Oi + qb * 4096;
         f32x16 st, dp = {};
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4) {  // S starts at -lse/scale of its 16 query rows
@@ -831,8 +875,8 @@ __global__ __launch_bounds__(64 * NB) void attn_bwd_pers(
         }
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
-          st = mfma32(rd_row(Qi, qb * 32 + (lane & 31), 2 * s + hh), kf[s], st);
-          dp = mfma32(rd_row(Oi, qb * 32 + (lane & 31), 2 * s + hh), vf[s], dp);
+          st = mfma32(rd_rowb(Qq, rb, s), kf[s], st);
+          dp = mfma32(rd_rowb(Oq, rb, s), vf[s], dp);
         }
         if (LAST && has_next) {  // kf / vf are dead from here on: the next unit's go straight in
           load_frag(kf, un, D);
@@ -865,8 +909,8 @@ __global__ __launch_bounds__(64 * NB) void attn_bwd_pers(
           const bf16x8 pf = pack8(pd, s2), df = pack8(st, s2);
 #pragma unroll
           for (int db = 0; db < 2; ++db) {
-            dv[db] = mfma32(pf, rd_tr(Oi, qb * 32 + 16 * s2, db * 32, lane), dv[db]);
-            dk[db] = mfma32(df, rd_tr(Qi, qb * 32 + 16 * s2, db * 32, lane), dk[db]);
+            dv[db] = mfma32(pf, rd_trb(Oq + s2 * 2048, tb, db), dv[db]);
+            dk[db] = mfma32(df, rd_trb(Qq + s2 * 2048, tb, db), dk[db]);
           }
         }
         if (LAST && cs_part) {  // this wave's keys: sum over all queries of dS
@@ -883,11 +927,13 @@ __global__ __launch_bounds__(64 * NB) void attn_bwd_pers(
         if (src < 0) src += NB;
         const char* So = Sall + src * 2048;
         const char* Ko = Kimg + src * 4096;
+        const TrB tb = tr_base(lane);
+        const int2 t64 = tr64_base(lane);
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
-          const bf16x8 sf = rd_tr64(So, 16 * s2, lane);
+          const bf16x8 sf = rd_tr64b(So + s2 * 1024, t64);
 #pragma unroll
-          for (int db = 0; db < 2; ++db) dq[db] = mfma32(rd_tr(Ko, 16 * s2, db * 32, lane), sf, dq[db]);
+          for (int db = 0; db < 2; ++db) dq[db] = mfma32(rd_trb(Ko + s2 * 2048, tb, db), sf, dq[db]);
         }
         if (i == PREP && has_next) prep_finish(un, cur ^ 1);
         if (LAST && cs_part) {
