@@ -234,7 +234,10 @@ __global__ __launch_bounds__(256) void ln_fwd8_kernel(const bf16* __restrict__ x
 }
 
 // partial layout as ln_bwd_kernel: ws[blk][3][D]
-template <int CPL>
+// G1: one gamma row (no LayerWiseNorm row groups): gamma is loaded into registers once per thread
+// instead of twice per row (12 of the 18 16-byte loads a row cost): 91 -> 72 us at ViT-B. (Loading
+// the next row's dy / x ahead of this row's math on top of that measured 82 us: not kept.)
+template <int CPL, bool G1 = false>
 __global__ __launch_bounds__(256) void ln_bwd8_kernel(const bf16* __restrict__ dy, long lddy, const bf16* __restrict__ x,
                                                       long ldx, const float* __restrict__ mean,
                                                       const float* __restrict__ rstd, const float* __restrict__ g,
@@ -262,9 +265,23 @@ __global__ __launch_bounds__(256) void ln_bwd8_kernel(const bf16* __restrict__ d
       if (res) rr[i] = ok ? *(const bf16x8*)(res + row * ldr + c * 8) : bf16x8{};
     }
   };
+  f32x4 gh[CPL][2];  // G1: this lane's gamma
+  if constexpr (G1) {
+#pragma unroll
+    for (int i = 0; i < CPL; ++i)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int c = l32 + 32 * i;
+        gh[i][h] = c < nc ? *(const f32x4*)(g + c * 8 + 4 * h) : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+  }
+  auto gam = [&](long gr, int i, int h) -> f32x4 {
+    if constexpr (G1) return gh[i][h];
+    else return *(const f32x4*)(g + gr + (l32 + 32 * i) * 8 + 4 * h);
+  };
   auto proc = [&](long row, const bf16x8(&dyr)[CPL], const bf16x8(&xr)[CPL], const bf16x8(&rr)[CPL]) {
     const float mu = mean[row], rs = rstd[row];
-    const long gr = grows > 1 ? ((row / rdiv) % grows) * D : 0;
+    const long gr = (!G1 && grows > 1) ? ((row / rdiv) % grows) * D : 0;
     // pass 1: the two row sums (xhat and dy*gamma are recomputed in pass 2: registers, not VALU,
     // bound this kernel's occupancy)
     float s1 = 0.f, s2 = 0.f;
@@ -276,7 +293,7 @@ __global__ __launch_bounds__(256) void ln_bwd8_kernel(const bf16* __restrict__ d
         for (int h = 0; h < 2; ++h) {
           const f32x4 dv = h ? hi4b(dyr[i]) : lo4b(dyr[i]);
           const f32x4 xh = ((h ? hi4b(xr[i]) : lo4b(xr[i])) - mu) * rs;
-          const f32x4 gy = dv * *(const f32x4*)(g + gr + c * 8 + 4 * h);
+          const f32x4 gy = dv * gam(gr, i, h);
           const f32x4 t = gy * xh;
           s1 += (gy[0] + gy[1]) + (gy[2] + gy[3]);
           s2 += (t[0] + t[1]) + (t[2] + t[3]);
@@ -295,7 +312,7 @@ __global__ __launch_bounds__(256) void ln_bwd8_kernel(const bf16* __restrict__ d
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           const f32x4 xh = ((h ? hi4b(xr[i]) : lo4b(xr[i])) - mu) * rs;
-          const f32x4 gy = (h ? hi4b(dyr[i]) : lo4b(dyr[i])) * *(const f32x4*)(g + gr + c * 8 + 4 * h);
+          const f32x4 gy = (h ? hi4b(dyr[i]) : lo4b(dyr[i])) * gam(gr, i, h);
           d[h] = (gy - s1 - xh * s2) * rs;
           if (res) d[h] += h ? hi4b(rr[i]) : lo4b(rr[i]);
         }
@@ -415,8 +432,13 @@ extern "C" int fer_layernorm_bwd(int dtype, const void* dy, int64_t lddy, const 
   static const bool old_ln = getenv("FERVIT_LN_OLD") != nullptr;  // A/B switch
   if (dtype == FER_BF16 && D % 8 == 0 && lddy % 8 == 0 && ldx % 8 == 0 && lddx % 8 == 0 && (!res || ldr % 8 == 0) &&
       !old_ln) {
+    static const bool g_rows = getenv("FERVIT_LN_BWD_GROWS") != nullptr;  // A/B: gamma loaded per row
+    const bool g1 = gamma_rows <= 1 && !g_rows;
 #define FER_LN_BWD8(C)                                                                                          \
-  hipLaunchKernelGGL(ln_bwd8_kernel<C>, dim3(nblk), dim3(256), 0, st, (const bf16*)dy, (long)lddy, (const bf16*)x, \
+  if (g1) FER_LN_BWD8K((ln_bwd8_kernel<C, true>))                                                               \
+  else FER_LN_BWD8K((ln_bwd8_kernel<C, false>))
+#define FER_LN_BWD8K(K)                                                                                         \
+  hipLaunchKernelGGL(K, dim3(nblk), dim3(256), 0, st, (const bf16*)dy, (long)lddy, (const bf16*)x, \
                      (long)ldx, mean, rstd, gamma, gamma_rows, row_div, (const bf16*)res, (long)ldr, (bf16*)dx,   \
                      (long)lddx, (bf16*)dx_drop, drop_thresh, drop_scale, seed, ws, (int)want, M, D);
     switch ((D + 255) / 256) {
@@ -426,6 +448,7 @@ extern "C" int fer_layernorm_bwd(int dtype, const void* dy, int64_t lddy, const 
       default: FER_LN_BWD8(4) break;
     }
 #undef FER_LN_BWD8
+#undef FER_LN_BWD8K
     int rc = hip_check("layernorm_bwd8");
     if (rc || !want) return rc;
     part_reduce(ws, nblk, 3L * D, 3 * D, D, dgamma, dbeta, dbias, accumulate, nullptr, st);
