@@ -372,7 +372,20 @@ __global__ __launch_bounds__(256) void ln_part_reduce_kernel(const float* __rest
   o[col] = accumulate ? o[col] + s : s;
 }
 
-static int ln_bwd_blocks(int M) { return std::max(1, std::min(ceil_div(M, 16), 1024)); }
+// One round of workgroups: two per CU (the kernel runs two waves per SIMD), each walking its rows
+// with the grid stride. 1024 blocks (two rounds) measured 71.5 us at ViT-B vs 63.5 us: the second
+// round's tail and twice the column partials for part_reduce. FERVIT_LN_BWD_BLOCKS overrides (A/B).
+static int ln_bwd_blocks(int M) {
+  static const int cap = [] {
+    if (const char* v = getenv("FERVIT_LN_BWD_BLOCKS")) return std::max(1, atoi(v));
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+    return 2 * n;
+  }();
+  return std::max(1, std::min(ceil_div(M, 16), cap));
+}
 
 }  // namespace fer
 
