@@ -403,7 +403,17 @@ extern "C" int fer_layernorm_fwd(int dtype, const void* x, int64_t ldx, const fl
   dim3 grid(ceil_div(M, 4));
   static const bool old_ln = getenv("FERVIT_LN_OLD") != nullptr;  // A/B switch
   if (dtype == FER_BF16 && D % 8 == 0 && ldx % 8 == 0 && ldy % 8 == 0 && !old_ln) {
-    const dim3 g8(std::max(1, std::min(ceil_div(M, 16), 2048)));  // two rows per half-wave in flight
+    // one round of workgroups (four per CU at this kernel's 4 waves per SIMD): 25.8 us at ViT-B vs
+    // 27.7 us with 2048 (two rounds); FERVIT_LN_FWD_BLOCKS overrides (A/B)
+    static const int fcap = [] {
+      if (const char* v = getenv("FERVIT_LN_FWD_BLOCKS")) return std::max(1, atoi(v));
+      int dev = 0, n = 0;
+      if (hipGetDevice(&dev) != hipSuccess ||
+          hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+        n = 256;
+      return 4 * n;
+    }();
+    const dim3 g8(std::max(1, std::min(ceil_div(M, 16), fcap)));  // two rows per half-wave in flight
 #define FER_LN_FWD8(C)                                                                                          \
   hipLaunchKernelGGL(ln_fwd8_kernel<C>, g8, dim3(256), 0, (hipStream_t)stream, (const bf16*)x, (long)ldx, gamma, \
                      beta, gamma_rows, row_div, (bf16*)y, (long)ldy, mean, rstd, M, D, eps);
