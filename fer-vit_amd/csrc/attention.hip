@@ -893,9 +893,11 @@ __global__ __launch_bounds__(64 * NB) void attn_bwd_pers(
           for (int j = 0; j < 4; ++j) {
             const int r = 4 * g4 + j;
             const float p = ex2(st[r] * sl2);
-            const bool kp = (mws >> acc_row(r, 0)) & 1u;
-            pd[r] = kp ? p : 0.f;
-            st[r] = p * fmaf(kp ? dp[r] : 0.f, dscale, -d4[j]);  // dS
+            // keep bit as an all-ones / zero mask (one v_bfe_i32): AND selects p / dp or +0.0,
+            // bit-identical to kp ? x : 0.f without a compare and two selects per element
+            const uint32_t km = (uint32_t)((int32_t)(mws << (31 - acc_row(r, 0))) >> 31);
+            pd[r] = __uint_as_float(__float_as_uint(p) & km);
+            st[r] = p * fmaf(__uint_as_float(__float_as_uint(dp[r]) & km), dscale, -d4[j]);  // dS
             cs += st[r];
           }
         }
