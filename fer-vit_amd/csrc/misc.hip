@@ -659,7 +659,34 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const
   const float step_size = sg.lr / bc1;
   const float bc2s = sqrtf(bc2);
   const float decay = 1.f - sg.lr * sg.weight_decay;
-  for (long j = blockIdx.x * 256L + threadIdx.x; j < sg.numel; j += (long)gridDim.x * 256L) {
+  // 16-byte accesses over the segment's multiple-of-4 head (segment offsets are 64-element aligned
+  // in FlatParams; checked per segment), then the per-element loop over the tail -- the same
+  // arithmetic per element either way
+  long j0 = 0;
+  if ((sg.offset & 3) == 0) {
+    j0 = sg.numel & ~3L;
+    for (long j = (blockIdx.x * 256L + threadIdx.x) * 4; j < j0; j += (long)gridDim.x * 1024L) {
+      const long i = sg.offset + j;
+      const f32x4 g4 = *(const f32x4*)(g + i);
+      f32x4 p4 = *(const f32x4*)(p + i), m4 = *(const f32x4*)(m + i), v4 = *(const f32x4*)(v + i);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float gr = g4[e] * sc;
+        float pv = p4[e] * decay;
+        const float mv = sg.beta1 * m4[e] + (1.f - sg.beta1) * gr;
+        const float vv = sg.beta2 * v4[e] + (1.f - sg.beta2) * gr * gr;
+        m4[e] = mv;
+        v4[e] = vv;
+        pv -= step_size * mv / (sqrtf(vv) / bc2s + sg.eps);
+        p4[e] = pv;
+      }
+      *(f32x4*)(m + i) = m4;
+      *(f32x4*)(v + i) = v4;
+      *(f32x4*)(p + i) = p4;
+      if (pb) *(bf16x4*)(pb + i) = bf16x4{(bf16)p4[0], (bf16)p4[1], (bf16)p4[2], (bf16)p4[3]};
+    }
+  }
+  for (long j = j0 + blockIdx.x * 256L + threadIdx.x; j < sg.numel; j += (long)gridDim.x * 256L) {
     const long i = sg.offset + j;
     const float gr = g[i] * sc;
     float pv = p[i] * decay;
@@ -1075,7 +1102,7 @@ extern "C" int fer_adamw(float* param, const float* grad, float* exp_avg, float*
                          const fer_adamw_segment* segs_device, int nsegs, int64_t max_seg_numel, float grad_scale,
                          const float* clip_coef, const uint64_t* step_add, fer_stream_t stream) {
   if (nsegs <= 0) return 0;
-  dim3 grid((unsigned)std::max<long>(1, std::min<long>((max_seg_numel + 255) / 256, 1024)), nsegs);
+  dim3 grid((unsigned)std::max<long>(1, std::min<long>((max_seg_numel + 1023) / 1024, 1024)), nsegs);
   hipLaunchKernelGGL(adamw_kernel, grid, dim3(256), 0, (hipStream_t)stream, param, grad, exp_avg, exp_avg_sq,
                      (bf16*)param_bf16, segs_device, grad_scale, clip_coef, step_add);
   return hip_check("adamw");
