@@ -180,6 +180,51 @@ def test_gemm_pre_gate_and_mul(act, dtype, p):
     assert rel_err(cs.cpu(), ref.sum(0)) < 2 * tol
 
 
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_gemm_8phase_epilogue_kinds(p):
+    """The 8-phase kernel's fixed-flag epilogues (csrc/gemm.hip epi_kind: EPI_STORE, EPI_GATE,
+    EPI_RES2, EPI_MUL2), forced through fer_gemm_set_config(8) on a ragged shape (partial last
+    tile row and column, K tail): the calls the post-norm layer makes (fervit/layers.py
+    PostNormLayerFn), each against an fp32 torch reference with the host-rebuilt keep mask."""
+    from fervit._lib import lib
+
+    o = ops()
+    M, N, K, seed = 1100, 520, 200, 4321
+    g = torch.Generator().manual_seed(11)
+    x, w = torch.randn(M, K, generator=g), torch.randn(N, K, generator=g) / math.sqrt(K)
+    b, r = torch.randn(N, generator=g), torch.randn(M, N, generator=g)
+    xr, wr, rr = (bf(t).float().cpu() for t in (x, w, r))
+    h = xr @ wr.t() + b
+    keep = keep_mask(seed, (M, N), p) if p > 0 else torch.ones(M, N, dtype=torch.bool)
+    lib().fer_gemm_set_config(8)
+    try:
+        # EPI_STORE: bias only (qkv fwd), and no epilogue at all (out-proj dgrad)
+        assert rel_err(o.linear_fwd(bf(x), bf(w), b.to(DEV)).cpu(), h) < 1e-2
+        assert rel_err(o.linear_fwd(bf(x), bf(w)).cpu(), xr @ wr.t()) < 1e-2
+        # EPI_GATE: fc1 fwd, GELU + dropout, pre = GELU'(h) * keep / (1 - p)
+        gate = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        y = o.linear_fwd(bf(x), bf(w), b.to(DEV), pre=gate, pre_gate=True, act="gelu", dropout=p, seed=seed,
+                         drop_ld=N)
+        hh = h.clone().requires_grad_(True)
+        a = torch.nn.functional.gelu(hh)
+        a.backward(torch.ones_like(a))
+        assert rel_err(y.cpu(), torch.where(keep, a.detach() / (1 - p), torch.zeros(()))) < 1e-2
+        assert rel_err(gate.cpu(), torch.where(keep, hh.grad / (1 - p), torch.zeros(()))) < 1e-2
+        # EPI_RES2: out-proj / fc2 fwd, bias + dropout + residual (and the residual-only dgrad form)
+        z = o.linear_fwd(bf(x), bf(w), b.to(DEV), res=bf(r), dropout=p, seed=seed, drop_ld=N)
+        assert rel_err(z.cpu(), torch.where(keep, h / (1 - p), torch.zeros(())) + rr) < 1e-2
+        z2 = o.linear_fwd(bf(x), bf(w), res=bf(r))
+        assert rel_err(z2.cpu(), xr @ wr.t() + rr) < 1e-2
+        # EPI_MUL2: fc2 dgrad through the gate, with the fused bias-gradient column sums
+        cs = torch.zeros(N, device=DEV)
+        dF = o.linear_fwd(bf(x), bf(w), aux=gate, aux_act="mul", colsum=cs)
+        ref = (xr @ wr.t()) * gate.float().cpu()
+        assert rel_err(dF.cpu(), ref) < 1e-2
+        assert rel_err(cs.cpu(), ref.sum(0)) < 2e-2
+    finally:
+        lib().fer_gemm_set_config(-1)
+
+
 def test_gemm_keep_rate():
     o = ops()
     M, N, K = 512, 1024, 64
