@@ -674,7 +674,7 @@ FER_DEV void tile_epilogue(const GemmArgs& g, const EpiArgs& e, AccT (&acc)[FN][
 // (q, r = 0..3); for MT=16, m = l&15 and n = 4(l>>4) + r.
 // Double-buffered BK=64 stages. Per K-step t: all LDS-DMA pieces of stage t+1, then SS
 // substeps of  ds_read(t, kk+1) | MFMAs(t, kk); then vmcnt(0) + s_barrier hands t+1 over.
-template <int BM, int BN, int WM, int WN, bool AKC, bool BKC, int MT>
+template <int BM, int BN, int WM, int WN, bool AKC, bool BKC, int MT, int EK = EPI_GEN>
 __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g, EpiArgs e) {
   typedef typename Acc<MT>::T AccT;
   constexpr int NW = WM * WN;
@@ -771,7 +771,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g, 
     if (acc[0][0][0] == 12345.f) g.ws[0] = 1.f;  // keep the MFMAs alive
     return;
   }
-  tile_epilogue<BM, BN, WM, WN, MT, (BM >= 256 ? 2 : 1), SMEM>(g, e, acc, smem, m0, n0, ks, wm, wn, lane);
+  tile_epilogue<BM, BN, WM, WN, MT, (BM >= 256 ? 2 : 1), SMEM, EK>(g, e, acc, smem, m0, n0, ks, wm, wn, lane);
 }
 
 // Ring variant: BK=32 stages in an NST-slot LDS ring, LDS-DMA issued NST-1 K-steps ahead and
@@ -1295,7 +1295,26 @@ static int launch_bf16(GemmArgs g, const EpiArgs& e, hipStream_t st) {
   g.tiles_m = (g.M + BM - 1) / BM;
   g.tiles_n = (g.N + BN - 1) / BN;
   dim3 grid(g.tiles_m * g.tiles_n, g.splits);
-  hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, WM, WN, AKC, BKC, MT>), grid, dim3(64 * WM * WN), 0, st, g, e);
+#define FER_BF16K(K) \
+  hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, WM, WN, AKC, BKC, MT, K>), grid, dim3(64 * WM * WN), 0, st, g, e)
+  // the 128^2 K-contiguous MT16 kernel (the small-grid configs: w+ latents, 48 px) also gets the
+  // fixed-flag epilogues (row operands through its LDS-DMA staging: the LDS-DMA kinds)
+  if constexpr (BM == 128 && BN == 128 && AKC && BKC && MT == 16) {
+    static const bool gen_only = getenv("FERVIT_EPI_GENERIC") != nullptr;
+    int ek = (g.partial || gen_only) ? EPI_GEN : epi_kind(e);
+    if (ek == EPI_RES2) ek = EPI_RES;
+    if (ek == EPI_MUL2) ek = EPI_MUL;
+    switch (ek) {
+      case EPI_STORE: FER_BF16K(EPI_STORE); break;
+      case EPI_GATE: FER_BF16K(EPI_GATE); break;
+      case EPI_RES: FER_BF16K(EPI_RES); break;
+      case EPI_MUL: FER_BF16K(EPI_MUL); break;
+      default: FER_BF16K(EPI_GEN); break;
+    }
+  } else {
+    FER_BF16K(EPI_GEN);
+  }
+#undef FER_BF16K
   return 0;
 }
 

@@ -180,10 +180,11 @@ def test_gemm_pre_gate_and_mul(act, dtype, p):
     assert rel_err(cs.cpu(), ref.sum(0)) < 2 * tol
 
 
+@pytest.mark.parametrize("cfg", [8, 3])
 @pytest.mark.parametrize("p", [0.0, 0.1])
-def test_gemm_8phase_epilogue_kinds(p):
+def test_gemm_8phase_epilogue_kinds(p, cfg):
     """The 8-phase kernel's fixed-flag epilogues (csrc/gemm.hip epi_kind: EPI_STORE, EPI_GATE,
-    EPI_RES2, EPI_MUL2), forced through fer_gemm_set_config(8) on a ragged shape (partial last
+    EPI_RES2, EPI_MUL2; and the 128^2 kernel's, cfg 3), forced through fer_gemm_set_config on a ragged shape (partial last
     tile row and column, K tail): the calls the post-norm layer makes (fervit/layers.py
     PostNormLayerFn), each against an fp32 torch reference with the host-rebuilt keep mask."""
     from fervit._lib import lib
@@ -196,7 +197,7 @@ def test_gemm_8phase_epilogue_kinds(p):
     xr, wr, rr = (bf(t).float().cpu() for t in (x, w, r))
     h = xr @ wr.t() + b
     keep = keep_mask(seed, (M, N), p) if p > 0 else torch.ones(M, N, dtype=torch.bool)
-    lib().fer_gemm_set_config(8)
+    lib().fer_gemm_set_config(cfg)
     try:
         # EPI_STORE: bias only (qkv fwd), and no epilogue at all (out-proj dgrad)
         assert rel_err(o.linear_fwd(bf(x), bf(w), b.to(DEV)).cpu(), h) < 1e-2
