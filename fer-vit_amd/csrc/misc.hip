@@ -174,6 +174,34 @@ __global__ __launch_bounds__(256) void tokens_bwd_kernel(const T* __restrict__ d
   }
   part[(long)blockIdx.y * cols + j] = s;
 }
+// 4 consecutive (token, d) columns per thread (D % 4 == 0: one token): 8/16-byte loads and
+// stores and one keep4 per 4 elements instead of a hash per element; same per-element values
+// and the same summation order over b as tokens_bwd_kernel (bit-identical partials).
+template <typename T>
+__global__ __launch_bounds__(256) void tokens_bwd4_kernel(const T* __restrict__ dt, T* __restrict__ demb, int B, int n,
+                                                          int D, uint32_t thr, float dscale, uint64_t seed,
+                                                          float* __restrict__ part, int bchunk) {
+  seed = step_seed(seed);
+  const int N = n + 1;
+  const long cols = (long)N * D;
+  const long j = (blockIdx.x * 256L + threadIdx.x) * 4;  // (token, d), d % 4 == 0
+  if (j >= cols) return;
+  const int tk = j / D, d = j - (long)tk * D;
+  const int b0 = blockIdx.y * bchunk, b1 = min(B, b0 + bchunk);
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
+  for (int b = b0; b < b1; ++b) {
+    const long i = (long)b * cols + j;
+    f32x4 g = load4<T>(dt + i);
+    if (thr) {
+      const uint32_t k = keep4(seed, (uint32_t)i, thr);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) g[r] = (k >> r) & 1 ? g[r] * dscale : 0.f;
+    }
+    s += g;
+    if (tk > 0 && demb) store4<T>(demb + ((long)b * n + tk - 1) * D + d, g);
+  }
+  *(f32x4*)(part + (long)blockIdx.y * cols + j) = s;
+}
 __global__ void tokens_bwd_final(const float* __restrict__ part, int nchunk, int N, int D, float* dcls, float* dpos,
                                  int accumulate) {
   const long j = blockIdx.x * 256L + threadIdx.x;
@@ -864,13 +892,23 @@ extern "C" int fer_tokens_bwd(int dtype, const void* dt, void* demb, float* dcls
   if (check_drop_range(drop_thresh, (long)B * N * D, "tokens_bwd: dropout over >= 2^32 elements")) return -1;
   const int bchunk = ceil_div(B, nch);
   hipStream_t st = (hipStream_t)stream;
-  dim3 grid(ceil_div((long)N * D, 256), nch);
-  if (dtype == FER_BF16)
-    hipLaunchKernelGGL(tokens_bwd_kernel<bf16>, grid, dim3(256), 0, st, (const bf16*)dt, (bf16*)demb, B, n, D,
-                       drop_thresh, drop_scale, seed, ws, bchunk);
-  else
-    hipLaunchKernelGGL(tokens_bwd_kernel<float>, grid, dim3(256), 0, st, (const float*)dt, (float*)demb, B, n, D,
-                       drop_thresh, drop_scale, seed, ws, bchunk);
+  if (D % 4 == 0) {
+    dim3 grid4(ceil_div((long)N * D / 4, 256), nch);
+    if (dtype == FER_BF16)
+      hipLaunchKernelGGL(tokens_bwd4_kernel<bf16>, grid4, dim3(256), 0, st, (const bf16*)dt, (bf16*)demb, B, n, D,
+                         drop_thresh, drop_scale, seed, ws, bchunk);
+    else
+      hipLaunchKernelGGL(tokens_bwd4_kernel<float>, grid4, dim3(256), 0, st, (const float*)dt, (float*)demb, B, n,
+                         D, drop_thresh, drop_scale, seed, ws, bchunk);
+  } else {
+    dim3 grid(ceil_div((long)N * D, 256), nch);
+    if (dtype == FER_BF16)
+      hipLaunchKernelGGL(tokens_bwd_kernel<bf16>, grid, dim3(256), 0, st, (const bf16*)dt, (bf16*)demb, B, n, D,
+                         drop_thresh, drop_scale, seed, ws, bchunk);
+    else
+      hipLaunchKernelGGL(tokens_bwd_kernel<float>, grid, dim3(256), 0, st, (const float*)dt, (float*)demb, B, n, D,
+                         drop_thresh, drop_scale, seed, ws, bchunk);
+  }
   if (dpos) part_reduce(ws, nch, (long)N * D, N * D, N * D, dpos, nullptr, nullptr, accumulate, nullptr, st);
   if (dcls) part_reduce(ws, nch, (long)N * D, D, D, dcls, nullptr, nullptr, accumulate, nullptr, st);
   return hip_check("tokens_bwd");

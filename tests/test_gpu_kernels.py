@@ -360,6 +360,28 @@ def test_colsum_and_tokens_and_head():
     assert torch.allclose(t.cpu().view(B, n + 1, D), ref, atol=1e-6)
 
 
+@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
+@pytest.mark.parametrize("D", [384, 6])
+def test_tokens_bwd_dropout(dtype, D):
+    """Gradient of the token assembly (cat(cls, patches) + pos, dropout): d(patches), d(cls) and
+    d(pos) against the host keep mask; D % 4 == 0 takes the 4-column kernel, D = 6 the per-element
+    one (csrc/misc.hip tokens_bwd4_kernel / tokens_bwd_kernel)."""
+    o = ops()
+    B, n, p, seed = 5, 9, 0.1, 777
+    N = n + 1
+    g = torch.Generator().manual_seed(21)
+    cast = bf if dtype == "bf16" else (lambda t: t.to(DEV))
+    dt = cast(torch.randn(B * N, D, generator=g))
+    dcls, dpos = torch.zeros(D, device=DEV), torch.zeros(N * D, device=DEV)
+    demb = o.tokens_bwd(dt, B, n, D, dcls, dpos, False, dropout=p, seed=seed)
+    keep = keep_mask(seed, (B, N * D), p).view(B, N, D)
+    gref = torch.where(keep, dt.float().cpu().view(B, N, D) / (1 - p), torch.zeros(()))
+    tol = 1e-2 if dtype == "bf16" else 1e-5
+    assert rel_err(demb.float().cpu().view(B, n, D), gref[:, 1:]) < tol
+    assert rel_err(dpos.cpu().view(N, D), gref.sum(0)) < tol
+    assert rel_err(dcls.cpu(), gref[:, 0].sum(0)) < tol
+
+
 def test_cross_entropy_matches_torch():
     o = ops()
     g = torch.Generator().manual_seed(9)
