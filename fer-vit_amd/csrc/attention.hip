@@ -1480,11 +1480,8 @@ extern "C" int64_t fer_attention_ws(int dtype, int B, int N, int H) {
 
 static bool pers_path(int dtype, int N, int dh) { return dtype == FER_BF16 && N <= 224 && dh <= 64; }
 static int64_t lse_floats(int B, int N, int H) { return ((int64_t)B * H * N + 63) / 64 * 64; }
-// A/B switch: persistent kernels walk a fixed blockIdx stride instead of the work queue
-static bool fixed_stride() {
-  static const bool f = getenv("FERVIT_FIXED_STRIDE") != nullptr;
-  return f;
-}
+// persistent kernels walk a fixed blockIdx stride instead of the work queue (fer_set_persistent_mode)
+static bool fixed_stride() { return fixed_stride_mode(); }
 static int n_cus() {
   static const int n = [] {
     int dev = 0, c = 0;
@@ -1545,6 +1542,7 @@ extern "C" int fer_attention_fwd(int dtype, const void* qkv, int64_t ld_qkv, voi
       FER_FPERS(1) FER_FPERS(2) FER_FPERS(3) FER_FPERS(4) FER_FPERS(5) FER_FPERS(6) FER_FPERS(7)
     }
 #undef FER_FPERS
+    wq_check_launch(st, wq);
   } else {
     const dim3 grid(B * H, (N + GEN_ROWS - 1) / GEN_ROWS);
     if (dh <= 64)
@@ -1617,6 +1615,7 @@ extern "C" int fer_attention_bwd(int dtype, const void* qkv, int64_t ld_qkv, con
       FER_PERS(1) FER_PERS(2) FER_PERS(3) FER_PERS(4) FER_PERS(5) FER_PERS(6) FER_PERS(7)
     }
 #undef FER_PERS
+    wq_check_launch(st, wq);
     int rc = hip_check("attention_bwd_bf16_pers");
     if (rc || !colsum) return rc;
     part_reduce(ws, B * nb, D3, D3, D3, colsum, nullptr, nullptr, colsum_accumulate, nullptr, st);

@@ -1,6 +1,7 @@
 // C ABI glue: error state and the GEMM entry point.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "fervit_internal.h"
@@ -23,7 +24,20 @@ int hip_check(const char* what) {
   return 0;
 }
 
+static int g_fixed_stride = -1;  // -1: FERVIT_FIXED_STRIDE decides on first use
+
+bool fixed_stride_mode() {
+  if (g_fixed_stride < 0) g_fixed_stride = getenv("FERVIT_FIXED_STRIDE") != nullptr ? 1 : 0;
+  return g_fixed_stride == 1;
+}
+
 }  // namespace fer
+
+extern "C" int fer_set_persistent_mode(int mode) {
+  if (mode < 0 || mode > 1) return fer::set_error("set_persistent_mode: mode must be 0 (work queue) or 1 (fixed stride)");
+  fer::g_fixed_stride = mode;
+  return 0;
+}
 
 extern "C" const char* fer_last_error(void) { return fer::g_err; }
 extern "C" const char* fer_version(void) { return "fervit-mi355x 0.1 (gfx950)"; }

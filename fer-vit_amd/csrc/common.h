@@ -362,31 +362,50 @@ FER_DEV int wq_claim(int* q, const uint32_t* base, int n) {
   const int nwg = ((int)gridDim.x - cls + 7) >> 3, items = (n - cls + 7) >> 3;
   return (long)t < (long)items - nwg ? cls + 8 * (nwg + (int)t) : -1;
 }
-// Host: the queue of this code object for a launch of `grid` workgroups over `n` items on `st`
-// (q = null: fixed stride). Advances the slot's bases by the claims the launch will make.
-static inline WqArgs wq_prepare_here(hipStream_t st, int grid, int n) {
+// Host state of this code object's queues: slots keyed by (device, stream) -- the counters live in
+// the device's own copy of fer_wq, whose address is looked up per device -- and a slot whose
+// launch failed is retired (the bases it advanced no longer match the counters), after which that
+// (device, stream) walks the fixed stride.
+struct WqHost {
   struct Slot {
     int* dev;
     uint32_t base[8];
+    bool dead;
   };
-  static std::mutex mu;
-  static std::map<hipStream_t, Slot> slots;
-  static int* pool = nullptr;
+  std::mutex mu;
+  std::map<std::pair<int, hipStream_t>, Slot> slots;
+  std::map<int, std::pair<int*, int>> pools;  // device -> (fer_wq on that device, slots used)
+};
+static inline WqHost& wq_host() {
+  static WqHost h;
+  return h;
+}
+// Host: the queue of this code object for a launch of `grid` workgroups over `n` items on `st`
+// (q = null: fixed stride). Advances the slot's bases by the claims the launch will make.
+static inline WqArgs wq_prepare_here(hipStream_t st, int grid, int n) {
   WqArgs a{};
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return a;
-  std::lock_guard<std::mutex> lk(mu);
-  if (!pool && hipGetSymbolAddress((void**)&pool, HIP_SYMBOL(fer_wq)) != hipSuccess) {
-    pool = nullptr;
-    return a;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return a;
+  WqHost& h = wq_host();
+  std::lock_guard<std::mutex> lk(h.mu);
+  auto pit = h.pools.find(dev);
+  if (pit == h.pools.end()) {
+    int* pool = nullptr;
+    if (hipGetSymbolAddress((void**)&pool, HIP_SYMBOL(fer_wq)) != hipSuccess) pool = nullptr;
+    pit = h.pools.emplace(dev, std::make_pair(pool, 0)).first;
   }
-  auto it = slots.find(st);
-  if (it == slots.end()) {
-    if ((int)slots.size() >= FER_WQ_SLOTS) return a;  // more streams than slots: fixed stride
-    Slot sl{pool + 8 * FER_WQ_PAD * (int)slots.size(), {}};
-    it = slots.emplace(st, sl).first;
+  if (!pit->second.first) return a;
+  const auto key = std::make_pair(dev, st);
+  auto it = h.slots.find(key);
+  if (it == h.slots.end()) {
+    if (pit->second.second >= FER_WQ_SLOTS) return a;  // more streams than slots: fixed stride
+    WqHost::Slot sl{pit->second.first + 8 * FER_WQ_PAD * pit->second.second++, {}, false};
+    it = h.slots.emplace(key, sl).first;
   }
-  Slot& sl = it->second;
+  WqHost::Slot& sl = it->second;
+  if (sl.dead) return a;
   a.q = sl.dev;
   for (int c = 0; c < 8; ++c) {
     a.base[c] = sl.base[c];
@@ -394,4 +413,15 @@ static inline WqArgs wq_prepare_here(hipStream_t st, int grid, int n) {
     sl.base[c] += (uint32_t)(std::max(0, items - nwg) + std::min(nwg, items));
   }
   return a;
+}
+// Host: call right after a work-queue launch; when the launch did not go out, the slot of
+// (current device, st) is retired (fixed stride from then on) instead of desynchronising silently.
+static inline void wq_check_launch(hipStream_t st, const WqArgs& a) {
+  if (!a.q || hipPeekAtLastError() == hipSuccess) return;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return;
+  WqHost& h = wq_host();
+  std::lock_guard<std::mutex> lk(h.mu);
+  auto it = h.slots.find(std::make_pair(dev, st));
+  if (it != h.slots.end()) it->second.dead = true;
 }

@@ -32,6 +32,9 @@ int set_step_ptr_attention(const uint64_t* p);
 int set_step_ptr_layernorm(const uint64_t* p);
 int set_step_ptr_misc(const uint64_t* p);
 int hip_check(const char* what);
+// persistent GEMM / attention kernels: walk a fixed blockIdx stride instead of the work queue
+// (fer_set_persistent_mode(1), or FERVIT_FIXED_STRIDE in the environment)
+bool fixed_stride_mode();
 int gemm_launch(const GemmDesc& d, const EpiArgs& e, hipStream_t st);
 inline int ceil_div(long a, long b);
 // out_k[c % seg] (+)= scale * sum_b part[b*ld + c]  (deterministic, misc.hip)

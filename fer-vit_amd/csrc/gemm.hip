@@ -282,6 +282,24 @@ FER_DEV void tile_of(int bid, int tiles_m, int tiles_n, int& tm, int& tn) {
   tn = w / gsize;
 }
 
+// Split-K launches (grid = tiles x splits): XCD-aware (split, tile) assignment. Blocks are dealt to
+// the XCDs round-robin by linear id (ids l and l + 8 share an XCD), so each XCD is given a
+// contiguous chunk of the split-major item list (split ks, tile t): the tiles of one split, which
+// read the same K rows of both operands in lockstep -- served by that XCD's L2 instead of once per
+// tile from the fabric (a weight gradient's A rows are shared by its tiles_n tiles, its B rows by
+// its tiles_m tiles). With the plain blockIdx.y = split order every XCD held tiles of every split.
+FER_DEV void split_tile_of(int tiles_m, int tiles_n, int& tm, int& tn, int& ks) {
+  const int T = tiles_m * tiles_n;
+  const int items = T * (int)gridDim.y;
+  const int lin = (int)blockIdx.y * (int)gridDim.x + (int)blockIdx.x;
+  const int xcd = lin & 7, q = items >> 3, r = items & 7;
+  const int item = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (lin >> 3);
+  ks = item / T;
+  const int t = item - ks * T;
+  tm = t % tiles_m;
+  tn = t / tiles_m;
+}
+
 // ------------------------------------------------------------- LDS-DMA stage
 constexpr int BK = 64;
 // KC image [rows][BKT k] (2*BKT-byte rows). BKT=64: chunk ^= (row>>1)&7. BKT=32 (4 rows per
@@ -692,10 +710,10 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g, 
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave % WM, wn = wave / WM;
 
-  int tm, tn;
-  tile_of(blockIdx.x, g.tiles_m, g.tiles_n, tm, tn);
+  int tm, tn, ks = 0;
+  if (gridDim.y > 1) split_tile_of(g.tiles_m, g.tiles_n, tm, tn, ks);
+  else tile_of(blockIdx.x, g.tiles_m, g.tiles_n, tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
-  const int ks = blockIdx.y;
   const int kbeg = ks * g.k_chunk;
   const int kend = min(g.K, kbeg + g.k_chunk);
   const int nk = (kend - kbeg + BK - 1) / BK;
@@ -799,10 +817,10 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_ring_kernel(GemmArgs g, 
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave % WM, wn = wave / WM;
 
-  int tm, tn;
-  tile_of(blockIdx.x, g.tiles_m, g.tiles_n, tm, tn);
+  int tm, tn, ks = 0;
+  if (gridDim.y > 1) split_tile_of(g.tiles_m, g.tiles_n, tm, tn, ks);
+  else tile_of(blockIdx.x, g.tiles_m, g.tiles_n, tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
-  const int ks = blockIdx.y;
   const int kbeg = ks * g.k_chunk;
   const int kend = min(g.K, kbeg + g.k_chunk);
   const int nk = (kend - kbeg + RBK - 1) / RBK;
@@ -907,7 +925,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_ring_kernel(GemmArgs g, 
 // waited for its own DMA pieces of it) and releases slot (t-1)%3, which is refilled with stage
 // t+2 right after it (two K-steps of DMA slack). Fragments of a K-step are read after the
 // barrier; the partner workgroup's waves fill the SIMD while they land.
-template <bool AKC, bool BKC>
+template <bool AKC, bool BKC, int EK = EPI_GEN>
 __global__ __launch_bounds__(256, 2) void gemm_pp_kernel(GemmArgs g, EpiArgs e) {
   typedef f32x4 AccT;
   constexpr int BM = 256, BN = 128, WM = 2, WN = 2, MT = 16, RBK = 32, NST = 3, NW = 4;
@@ -917,10 +935,10 @@ __global__ __launch_bounds__(256, 2) void gemm_pp_kernel(GemmArgs g, EpiArgs e) 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave % WM, wn = wave / WM;
-  int tm, tn;
-  tile_of(blockIdx.x, g.tiles_m, g.tiles_n, tm, tn);
+  int tm, tn, ks = 0;
+  if (gridDim.y > 1) split_tile_of(g.tiles_m, g.tiles_n, tm, tn, ks);
+  else tile_of(blockIdx.x, g.tiles_m, g.tiles_n, tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
-  const int ks = blockIdx.y;
   const int kbeg = ks * g.k_chunk;
   const int kend = min(g.K, kbeg + g.k_chunk);
   const int nk = (kend - kbeg + RBK - 1) / RBK;
@@ -965,14 +983,32 @@ __global__ __launch_bounds__(256, 2) void gemm_pp_kernel(GemmArgs g, EpiArgs e) 
       for (int i = 0; i < FN; ++i) acc[i][j] = mfma<MT>(bfr[i], af[j], acc[i][j]);
   }
   __syncthreads();  // every wave's fragment reads are done: the ring becomes epilogue staging
-  tile_epilogue<BM, BN, WM, WN, MT, 2, NST * STAGE>(g, e, acc, smem, m0, n0, ks, wm, wn, lane);
+  tile_epilogue<BM, BN, WM, WN, MT, 2, NST * STAGE, EK>(g, e, acc, smem, m0, n0, ks, wm, wn, lane);
 }
 
 template <bool AKC, bool BKC>
 static int launch_pp(GemmArgs g, const EpiArgs& e, hipStream_t st) {
   g.tiles_m = (g.M + 255) / 256;
   g.tiles_n = (g.N + 127) / 128;
-  hipLaunchKernelGGL((gemm_pp_kernel<AKC, BKC>), dim3(g.tiles_m * g.tiles_n, g.splits), dim3(256), 0, st, g, e);
+  const dim3 grid(g.tiles_m * g.tiles_n, g.splits);
+  // fixed-flag epilogue kinds as in the 8-phase kernel (K-contiguous operands, no split-K)
+  static const bool gen_only = getenv("FERVIT_EPI_GENERIC") != nullptr;
+  const int ek = (AKC && BKC && !g.partial && !gen_only) ? epi_kind(e) : EPI_GEN;
+#define FER_PPK(K) hipLaunchKernelGGL((gemm_pp_kernel<AKC, BKC, K>), grid, dim3(256), 0, st, g, e)
+  if constexpr (AKC && BKC) {
+    switch (ek) {
+      case EPI_STORE: FER_PPK(EPI_STORE); break;
+      case EPI_GATE: FER_PPK(EPI_GATE); break;
+      case EPI_RES: FER_PPK(EPI_RES); break;
+      case EPI_MUL: FER_PPK(EPI_MUL); break;
+      case EPI_RES2: FER_PPK(EPI_RES2); break;
+      case EPI_MUL2: FER_PPK(EPI_MUL2); break;
+      default: FER_PPK(EPI_GEN); break;
+    }
+  } else {
+    FER_PPK(EPI_GEN);
+  }
+#undef FER_PPK
   return 0;
 }
 
@@ -1341,10 +1377,10 @@ static int launch_8ph(GemmArgs g, const EpiArgs& e, hipStream_t st) {
   static const bool persist = getenv("FERVIT_GEMM_NOPERSIST") == nullptr;  // A/B switch
   const int ntiles = g.tiles_m * g.tiles_n;
   const int gx = persist ? std::min(ntiles, std::max(8, ncu / 8 * 8)) : ntiles;
-  static const bool fixed = getenv("FERVIT_FIXED_STRIDE") != nullptr;  // A/B switch
   g.tq = nullptr;
-  if (persist && !fixed && g.splits == 1) {
-    const WqArgs w = wq_prepare_here(st, gx, ntiles);
+  WqArgs w{};
+  if (persist && !fixed_stride_mode() && g.splits == 1) {
+    w = wq_prepare_here(st, gx, ntiles);
     g.tq = w.q;
     for (int c = 0; c < 8; ++c) g.tq_base[c] = w.base[c];
   }
@@ -1375,6 +1411,7 @@ static int launch_8ph(GemmArgs g, const EpiArgs& e, hipStream_t st) {
   }
 #undef FER_8PH_K
 #undef FER_8PH
+  wq_check_launch(st, w);
   return 0;
 }
 

@@ -47,6 +47,7 @@ class ImageAug(C.Structure):
 SIGNATURES = {
     "fer_gemm": (i32, [C.POINTER(GemmDesc), C.POINTER(Epilogue), vp]),
     "fer_gemm_set_config": (i32, [i32]),
+    "fer_set_persistent_mode": (i32, [i32]),
     "fer_gemm_colsum_ws": (i64, [i32, i32]),
     "fer_layernorm_fwd": (i32, [i32, vp, i64, fp, fp, i32, i32, vp, i64, fp, fp, i32, i32, f32, vp]),
     "fer_layernorm_bwd_ws": (i64, [i32, i32]),

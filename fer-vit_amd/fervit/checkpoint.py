@@ -37,8 +37,7 @@ def load_checkpoint(path: str, model: Optional[torch.nn.Module] = None,
                     optimizer: Optional[torch.optim.Optimizer] = None) -> Dict[str, Any]:
     """Load a checkpoint written by save_checkpoint or by the reference's ExperimentLogger
     ('model_state_dict' or the older 'model_state' key, `eval/evaluate_model.py:117-122`)."""
-    with torch.serialization.safe_globals(_numpy_safe_globals()):
-        ckpt = torch.load(path, map_location="cpu", weights_only=True)
+    ckpt = _safe_load(path)
     if model is not None:
         sd = ckpt.get("model_state_dict", ckpt.get("model_state"))
         if sd is None:
@@ -49,20 +48,42 @@ def load_checkpoint(path: str, model: Optional[torch.nn.Module] = None,
     return ckpt
 
 
+def _safe_load(path: str):
+    """torch.load(weights_only=True) with the numpy reconstructors allow-listed: through the
+    `safe_globals` context manager where torch has it, else the process-wide
+    `add_safe_globals` (torch 2.4), else a plain weights_only load (older torch: tensor-only
+    checkpoints still load; numpy-valued metrics are then refused by torch, never unpickled)."""
+    ser = torch.serialization
+    g = _numpy_safe_globals()
+    if hasattr(ser, "safe_globals"):
+        with ser.safe_globals(g):
+            return torch.load(path, map_location="cpu", weights_only=True)
+    if hasattr(ser, "add_safe_globals"):
+        ser.add_safe_globals(g)
+    return torch.load(path, map_location="cpu", weights_only=True)
+
+
 def _numpy_safe_globals():
     """numpy scalar / array reconstructors (numpy 2 and numpy 1.x module paths) and the dtype
     classes a pickled numpy value references. These only rebuild values; none runs user code
     (an object-dtype array would still need its element classes, which stay disallowed)."""
     import numpy as np
-    import numpy.dtypes as ndt
-    from numpy._core.multiarray import _reconstruct, scalar
+
+    try:  # numpy >= 2
+        from numpy._core.multiarray import _reconstruct, scalar
+    except ImportError:  # numpy 1.x (the reference allows numpy >= 1.21)
+        from numpy.core.multiarray import _reconstruct, scalar
+    try:
+        import numpy.dtypes as ndt  # numpy >= 1.25
+    except ImportError:
+        ndt = None
 
     g = [scalar, (scalar, "numpy.core.multiarray.scalar"), _reconstruct,
          (_reconstruct, "numpy.core.multiarray._reconstruct"), np.ndarray, np.dtype]
     for name in ("Int8DType", "Int16DType", "Int32DType", "Int64DType", "UInt8DType", "UInt16DType", "UInt32DType",
                  "UInt64DType", "Float16DType", "Float32DType", "Float64DType", "BoolDType", "LongLongDType",
                  "LongDType"):
-        if hasattr(ndt, name):
+        if ndt is not None and hasattr(ndt, name):
             g.append(getattr(ndt, name))
     return g
 

@@ -10,7 +10,8 @@ What changes under replay, and how it stays correct:
     a device step counter into every seed (fer_set_step_counter), and the first node of the
     graph advances that counter (fer_step_advance), so every replay draws fresh masks;
   * AdamW: the segment table is uploaded once and the bias-correction step becomes
-    host step + *counter (FusedAdamW.freeze_for_graph);
+    host step + *counter (FusedAdamW.freeze_for_graph); hyper-parameters a scheduler changes
+    between replays are rewritten into that table before the next replay (sync_graph_hparams);
   * inputs: replays read the tensors captured by the step function -- copy each new batch
     into them (static input buffers), as with any CUDA/HIP graph;
   * memory: activations live in the graph's private pool; the library workspaces are sized by
@@ -49,14 +50,21 @@ class StepGraph:
         check(lib().fer_set_step_counter(self.counter.data_ptr()), "set_step_counter")
         self.opt.freeze_for_graph(self.counter)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        # captured on the warm-up stream: the library's per-stream workspaces (ops.WS) sized by
+        # the warm-up are the ones the captured launches use (no allocation under capture)
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.graph(g, stream=side):
             check(lib().fer_step_advance(self.counter.data_ptr(), ops.stream()), "step_advance")
             self.out = self.step_fn()
+        torch.cuda.current_stream().wait_stream(side)
         self.graph = g
         return self
 
     def replay(self) -> torch.Tensor:
-        """One training step; returns the (device) loss tensor of this replay."""
+        """One training step; returns the (device) loss tensor of this replay. A learning-rate
+        (or other hyper-parameter) change made since the last replay -- an LR scheduler's
+        step -- is written into the captured AdamW segment table first."""
+        self.opt.sync_graph_hparams()
         self.graph.replay()
         return self.out
 

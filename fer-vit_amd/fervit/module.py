@@ -51,7 +51,13 @@ class FerModule(nn.Module):
     def fer_flat(self) -> FlatParams:
         owner = self._fer_owner() if self._fer_owner is not None else None
         if owner is not None and owner._fer_flat is not None:
-            return owner._fer_flat
+            flat = owner._fer_flat
+            if not flat.owner_active:
+                # a child module run on its own (e.g. `model.backbone(x)`), not inside the owner's
+                # forward: start a pass so the bf16 shadow re-checks the parameters' versions
+                # (they may have been changed in place since the owner's last pass)
+                flat.begin_pass()
+            return flat
         if self._fer_flat is not None:
             self._fer_flat.begin_pass()
             return self._fer_flat
@@ -61,7 +67,19 @@ class FerModule(nn.Module):
                 raise RuntimeError("fervit: module has no parameters")
             if not params[0].is_cuda:
                 raise RuntimeError("fervit: move the model to a ROCm device first (no CPU path)")
-            object.__setattr__(self, "_fer_flat", FlatParams(params))
+            flat = FlatParams(params)
+            object.__setattr__(self, "_fer_flat", flat)
+            for h in getattr(self, "_fer_hooks", ()):
+                h.remove()
+
+            def _enter(_m, _inp, flat=flat):
+                flat.owner_active = True
+
+            def _leave(_m, _inp, _out, flat=flat):
+                flat.owner_active = False
+
+            object.__setattr__(self, "_fer_hooks", (self.register_forward_pre_hook(_enter),
+                                                    self.register_forward_hook(_leave, always_call=True)))
             ref = weakref.ref(self)
             for m in self.modules():
                 if m is not self and isinstance(m, FerModule):

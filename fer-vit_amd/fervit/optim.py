@@ -30,6 +30,14 @@ class FusedAdamW(torch.optim.Optimizer):
         self._step_counter: Optional[torch.Tensor] = None  # graph mode (freeze_for_graph)
         self._frozen = None
 
+    def zero_grad(self, set_to_none: bool = True):
+        """torch semantics, plus: a clip coefficient left by clip_grad_norm_ for a step that was
+        then skipped is dropped here, so it cannot scale the next step's unrelated gradients."""
+        super().zero_grad(set_to_none=set_to_none)
+        self.clip_coef = None
+        if self.model is not None and getattr(self.model, "_fer_clip_coef", None) is not None:
+            self.model._fer_clip_coef = None
+
     def _bind(self):
         flat = self.model.fer_flat() if self.model is not None else None
         if flat is None:
@@ -91,11 +99,42 @@ class FusedAdamW(torch.optim.Optimizer):
     def freeze_for_graph(self, counter: torch.Tensor) -> None:
         """Graph mode (fervit.graph.StepGraph): the segment table is uploaded once and the
         AdamW step of every parameter becomes (its host step count now) + *counter, the device
-        step counter the captured step advances. Call after the eager warm-up steps."""
+        step counter the captured step advances. Call after the eager warm-up steps. A later
+        change of a group's lr / weight_decay / betas / eps (an LR scheduler's step) is written
+        into the same device table before the next replay (sync_graph_hparams)."""
         flat = self._bind()
         segs, maxn = self._segments(flat, bump=False)
         self._frozen = (self._upload(segs, flat), len(segs), maxn)
+        # group of every segment (same walk as _segments), to rebuild the table with new hparams
+        self._frozen_groups = [gi for gi, g in enumerate(self.param_groups) for p in g["params"] if p.grad is not None]
+        self._frozen_segs = segs
+        self._frozen_hp = self._hparams()
         self._step_counter = counter
+
+    def _hparams(self):
+        return [(g["lr"], g["weight_decay"], tuple(g["betas"]), g["eps"]) for g in self.param_groups]
+
+    def sync_graph_hparams(self) -> bool:
+        """Graph mode: if any group's hyper-parameters changed since the table was uploaded (e.g.
+        CosineAnnealingLR.step() at an epoch end, `train/train_latent_vit_v2.py:368-370`), rewrite
+        the captured segment table in place (a stream-ordered copy ahead of the replay: the
+        replayed AdamW node reads it from device memory). Returns True when it rewrote it."""
+        if self._frozen is None:
+            return False
+        hp = self._hparams()
+        if hp == self._frozen_hp:
+            return False
+        if len(hp) != len(self._frozen_hp):
+            raise RuntimeError("FusedAdamW: param groups changed under a captured StepGraph; release() it first")
+        segs = []
+        for gi, (off, n, _lr, _wd, _b1, _b2, _eps, step) in zip(self._frozen_groups, self._frozen_segs):
+            g = self.param_groups[gi]
+            b1, b2 = g["betas"]
+            segs.append((off, n, g["lr"], g["weight_decay"], b1, b2, g["eps"], step))
+        self._frozen[0].copy_(self._upload(segs, self._flat), non_blocking=True)
+        self._frozen_segs = segs
+        self._frozen_hp = hp
+        return True
 
     def unfreeze(self) -> None:
         """Leave graph mode (StepGraph.release): the replays' device step count is folded into
@@ -190,11 +229,13 @@ def clip_grad_norm_(model, max_norm: float, sq_scale: float = 1.0, optimizer: Op
     handed to the fused optimizer (`optimizer.clip_coef`, and `model._fer_clip_coef` for a
     FusedAdamW bound to this model), whose next step multiplies every gradient by it -- the
     same arithmetic as torch's in-place `g *= coef` followed by AdamW. Returns the total norm
-    (device scalar), as torch does. Parameters without a gradient hold zeros in the flat buffer
-    (it starts zeroed and only gradient writes touch it), so they add nothing, like torch's
-    skip of `p.grad is None`."""
+    (device scalar), as torch does. Like torch, only parameters with a gradient count: a
+    parameter whose `.grad` is None (never written, or dropped by zero_grad(set_to_none=True)
+    after an earlier backward wrote its slot) contributes nothing -- FlatParams.settle_grads
+    zeroes such stale slots and copies foreign `.grad` tensors into the flat buffer first."""
     flat = model.fer_flat()
     runtime.WGRAD.sync()
+    flat.settle_grads()
     out = torch.empty(2, dtype=torch.float32, device=flat.grad.device)
     ws = ops.WS.get(4 * 4096, flat.grad.device, slot=3)
     check(lib().fer_sumsq(flat.grad.data_ptr(), flat.numel, out.data_ptr(), ws.data_ptr(), ws.numel() * 4,

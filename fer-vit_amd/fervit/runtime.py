@@ -77,6 +77,8 @@ class FlatParams:
         self.half_t: Optional[torch.Tensor] = None  # transposed bf16 copies of the 2-D params
         self._tsegs: Optional[torch.Tensor] = None
         self._ttiles = 0
+        self._written = set()  # ids of parameters whose grad slot a backward has written
+        self.owner_active = False  # inside the owning module's forward (FerModule hooks)
         with torch.no_grad():
             for p in self.params:
                 v = self.view(p)
@@ -166,10 +168,27 @@ class FlatParams:
         return self.half_t[o:o + p.numel()].view(c, r)
 
     # ---- gradient side channel
+    def settle_grads(self) -> None:
+        """Make the flat grad buffer equal torch's view of the gradients before a whole-buffer
+        reduction (clip_grad_norm_): a slot written in an earlier backward whose parameter's
+        `.grad` is now None is zeroed (torch skips such parameters), and a foreign `.grad`
+        tensor (assigned by user code) is copied into its slot."""
+        for p in self.params:
+            g = p.grad
+            if g is None:
+                if id(p) in self._written:
+                    self.grad_views[id(p)].zero_()
+                    self._written.discard(id(p))
+            elif g.data_ptr() != self.grad_views[id(p)].data_ptr():
+                with torch.no_grad():
+                    self.grad_views[id(p)].copy_(g)
+                self._written.add(id(p))
+
     def grad_target(self, p) -> (torch.Tensor, bool):
         """(view to write p's gradient into, accumulate?) following torch semantics:
         p.grad None -> overwrite; p.grad is our view -> accumulate; foreign tensor ->
         copy it into the view, then accumulate."""
+        self._written.add(id(p))
         gv = self.grad_views[id(p)]
         g = p.grad
         if g is None:

@@ -81,9 +81,15 @@ int fer_gemm(const fer_gemm_desc* d, const fer_epilogue* e, fer_stream_t stream)
 int64_t fer_gemm_colsum_ws(int M, int N);
 
 /* Tuning/testing hook (no reference counterpart): force the bf16 GEMM tile configuration for
- * every later fer_gemm call of the process. -1 = automatic (default); 0..9 = fixed kernel
- * (see csrc/gemm.hip). Results are identical up to fp32 summation order. */
+ * every later fer_gemm call of the process. -1 = automatic (default); 0..10 = fixed kernel
+ * (see csrc/gemm.hip dispatch_tile). Results are identical up to fp32 summation order. */
 int fer_gemm_set_config(int cfg);
+
+/* Testing / A/B hook (no reference counterpart): the persistent kernels (8-phase GEMM, persistent
+ * attention; one workgroup per CU) take their items from a per-(device, stream) work queue
+ * (mode 0, default) or walk a fixed blockIdx stride (mode 1; FERVIT_FIXED_STRIDE=1 sets it at
+ * start-up). Results are bit-identical between the modes. */
+int fer_set_persistent_mode(int mode);
 
 /* LayerNorm forward over rows of x [M][D] (nn.LayerNorm, biased variance;
  * post-norm `nn.TransformerEncoderLayer` norm1/norm2, heads `image_vit.py:162-163`,

@@ -34,3 +34,25 @@ def keep_mask(seed: int, shape, p: float, base: int = 0) -> torch.Tensor:
     h = fer_hash(seed, idx >> np.uint64(1))
     u = (h >> ((idx & np.uint64(1)) * np.uint64(16))) & np.uint64(0xFFFF)
     return torch.from_numpy((u >= np.uint64(thresh(p))).reshape(shape))
+
+
+def keep_mask_torch(seed: int, shape, p: float, device="cuda") -> torch.Tensor:
+    """keep_mask computed with int64 torch ops on `device` (large masks: a GPU test's attention
+    dropout over B*H*N*N elements). 32-bit products are split into 16-bit halves so no int64
+    product overflows."""
+    n = int(np.prod(shape))
+    m32 = 0xFFFFFFFF
+    idx = torch.arange(n, dtype=torch.int64, device=device) & m32
+
+    def mul32(x, c):
+        return ((x * (c & 0xFFFF)) + (((x * (c >> 16)) & 0xFFFF) << 16)) & m32
+
+    x = ((idx >> 1) ^ (seed & m32)) + ((seed >> 32) & m32)
+    x &= m32
+    x ^= x >> 16
+    x = mul32(x, 0x7FEB352D)
+    x ^= x >> 15
+    x = mul32(x, 0x846CA68B)
+    x ^= x >> 16
+    u = (x >> ((idx & 1) * 16)) & 0xFFFF
+    return (u >= thresh(p)).reshape(shape)

@@ -118,3 +118,47 @@ def test_release_folds_replays_into_step_count():
     for pa, pb in zip(ma.parameters(), mb.parameters()):
         assert (pa.detach() - pb.detach()).abs().max().item() <= 1e-6
     assert {int(v["step"]) for v in ob.state_dict()["state"].values()} == {8}
+
+
+def test_graph_replay_follows_lr_scheduler():
+    """An LR scheduler stepped between replays (`train/train_latent_vit_v2.py:368-370`: one
+    scheduler.step() per epoch) changes the lr the captured AdamW node uses: the segment table is
+    rewritten before the next replay (FusedAdamW.sync_graph_hparams), so graph and eager runs with
+    the same schedule stay equal -- and differ from a run whose lr never changes."""
+    from fervit.graph import StepGraph
+    from fervit.optim import FusedAdamW
+
+    x, y = batch()
+    runs = []
+    for mode in ("eager", "graph", "graph-const-lr"):
+        m, crit = make(0.0)
+        o = FusedAdamW(m.parameters(), lr=2e-3, weight_decay=0.05, model=m)
+        sched = torch.optim.lr_scheduler.CosineAnnealingLR(o, T_max=4)
+
+        def step():
+            o.zero_grad(set_to_none=True)
+            loss = crit(m(x), y)
+            loss.backward()
+            o.step()
+            return loss
+
+        if mode == "eager":
+            for _ in range(2):  # the graph runs' warm-up steps
+                step()
+        else:
+            sg = StepGraph(step, o, warmup=2).capture()
+        for epoch in range(4):
+            for _ in range(2):
+                step() if mode == "eager" else sg.replay()
+            if mode != "graph-const-lr":
+                sched.step()
+        if mode != "eager":
+            sg.release()
+        torch.cuda.synchronize()
+        runs.append([p.detach().clone() for p in m.parameters()])
+        if mode != "graph-const-lr":
+            assert o.param_groups[0]["lr"] < 1e-4  # the schedule ran (cosine to ~0 at T_max)
+    eager, graph, const = runs
+    for pa, pb in zip(eager, graph):
+        assert (pa - pb).abs().max().item() <= 1e-6
+    assert max((pa - pc).abs().max().item() for pa, pc in zip(eager, const)) > 1e-4

@@ -344,6 +344,99 @@ def test_attention_fwd_bwd(N, H, dh, dtype, p):
     assert torch.equal(dqkv2, dqkv) and torch.equal(cs2, cs)
 
 
+@pytest.mark.parametrize("N,H,dh,B", [(197, 12, 64, 64), (19, 8, 64, 128)])
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_attention_persistent_multi_unit(N, H, dh, B, p):
+    """The headline configuration's persistent attention path with several (batch, head) units per
+    workgroup: B*H = 768 / 1024 units on <= 256 workgroups, so every workgroup walks >= 3 units
+    (next-unit K/V prefetch into the second LDS buffer, work-queue claims). Forward output, lse,
+    the stored keep bits, dQ/dK/dV and the fused in_proj bias gradient against a torch fp32
+    reference on the GPU, under the work queue (mode 0) and the fixed stride (mode 1), which must
+    also agree bit for bit (csrc/attention.hip attn_fwd_pers / attn_bwd_pers)."""
+    from dropmask import keep_mask_torch
+    from fervit._lib import lib
+
+    o = ops()
+    D = H * dh
+    seed = 777 + N
+    g = torch.Generator(device=DEV).manual_seed(B * N + H)
+    qkv = torch.randn(B * N, 3 * D, device=DEV, generator=g).to(torch.bfloat16)
+    dout = torch.randn(B * N, D, device=DEV, generator=g).to(torch.bfloat16)
+    keep = keep_mask_torch(seed, (B, H, N, N + (N & 1)), p)[..., :N] if p > 0 else None
+    qr = qkv.float().requires_grad_(True)
+    ref, lse_ref = attn_ref(qr, B, N, H, dh, keep, p)
+    ref.backward(dout.float())
+    results = []
+    for mode in (0, 1):
+        lib().fer_set_persistent_mode(mode)
+        try:
+            out = torch.empty(B * N, D, device=DEV, dtype=torch.bfloat16)
+            saved = o.attention_saved(qkv, B, N, H, dh, dropout=p)
+            o.attention_fwd(qkv, out, saved, B, N, H, dh, dropout=p, seed=seed)
+            dqkv = torch.empty_like(qkv)
+            cs = torch.zeros(3 * D, device=DEV)
+            o.attention_bwd(qkv, out, dout, saved, dqkv, B, N, H, dh, dropout=p, seed=seed, colsum=cs)
+            torch.cuda.synchronize()
+        finally:
+            lib().fer_set_persistent_mode(0)
+        assert rel_err(out, ref) < 2e-2, mode
+        assert (saved[:B * H * N] - lse_ref.reshape(-1)).abs().max().item() < 2e-2, mode
+        if p > 0:
+            nb = (N + 31) // 32
+            off = (B * H * N + 63) // 64 * 64
+            words = saved[off:off + B * H * nb * nb * 32].view(torch.int32).view(B * H, nb, nb, 32).to(torch.int64)
+            words &= 0xFFFFFFFF
+            bits = (words[..., None] >> torch.arange(32, device=DEV)) & 1  # [bh][kb][qb][j][qi]
+            got = bits.permute(0, 2, 4, 1, 3).reshape(B * H, nb * 32, nb * 32).bool()[:, :N, :N]
+            assert torch.equal(got, keep.reshape(B * H, N, N)), mode
+        for j, name in enumerate("qkv"):
+            assert rel_err(dqkv[:, j * D:(j + 1) * D], qr.grad[:, j * D:(j + 1) * D]) < 4e-2, (mode, name)
+        assert rel_err(cs, qr.grad.sum(0)) < 4e-2, mode
+        results.append((out, saved, dqkv, cs))
+    for a, b in zip(*results):
+        assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
+def test_head_dropout_keep_mask(dtype):
+    """Classification head with train-mode dropout between its LayerNorm and Linear (the hybrid
+    head `hybrid_latent_vit.py:110-114`: LayerNorm -> Dropout(0.1) -> Linear) through
+    fer_head_fwd / fer_head_bwd, against torch with the host-rebuilt keep mask (element index
+    b*D + d): logits, d(CLS rows), zeroed other rows, and the LN / Linear parameter gradients."""
+    o = ops()
+    B, N, D, C, p, seed = 37, 5, 768, 7, 0.1, 31337
+    g = torch.Generator().manual_seed(3)
+    cast = bf if dtype == "bf16" else (lambda t: t.to(DEV))
+    t = cast(torch.randn(B * N, D, generator=g))
+    lnw, lnb = 1 + 0.1 * torch.randn(D, generator=g), 0.1 * torch.randn(D, generator=g)
+    W, b = torch.randn(C, D, generator=g) / math.sqrt(D), torch.randn(C, generator=g)
+    dl = torch.randn(B, C, generator=g)
+    logits, stats = o.head_fwd(t, N, lnw.to(DEV), lnb.to(DEV), 1e-5, W.to(DEV), b.to(DEV), B, dropout=p, seed=seed)
+    keep = keep_mask(seed, (B, D), p)
+    tr = t.float().cpu().requires_grad_(True)
+    P = [x.clone().requires_grad_(True) for x in (lnw, lnb, W, b)]
+    cls = tr.view(B, N, D)[:, 0]
+    h = torch.nn.functional.layer_norm(cls, (D,), P[0], P[1], 1e-5)
+    hd = torch.where(keep, h / (1 - p), torch.zeros(()))
+    ref = hd @ P[2].t() + P[3]
+    tol = 1e-2 if dtype == "bf16" else 1e-5
+    assert rel_err(logits.cpu(), ref) < tol
+    ref.backward(dl)
+    grads = [torch.zeros_like(x, device=DEV) for x in (lnw, lnb, W, b)]
+    dt = o.head_bwd(t, N, lnw.to(DEV), lnb.to(DEV), W.to(DEV), stats, dl.to(DEV), B, grads, False, dropout=p,
+                    seed=seed)
+    assert rel_err(dt.float().cpu(), tr.grad) < tol
+    assert torch.count_nonzero(dt.view(B, N, D)[:, 1:]).item() == 0
+    for got, want in zip(grads, P):
+        assert rel_err(got.cpu(), want.grad) < tol
+    # a dropped feature of sample b passes no gradient to its LN output: d(ln_b) restricted to one
+    # sample (B = 1 launch) is zero exactly where that sample's feature was dropped
+    g1 = [torch.zeros_like(x, device=DEV) for x in (lnw, lnb, W, b)]
+    _, st1 = o.head_fwd(t[:N], N, lnw.to(DEV), lnb.to(DEV), 1e-5, W.to(DEV), b.to(DEV), 1, dropout=p, seed=seed)
+    o.head_bwd(t[:N], N, lnw.to(DEV), lnb.to(DEV), W.to(DEV), st1, dl[:1].to(DEV), 1, g1, False, dropout=p, seed=seed)
+    assert torch.equal(g1[1].cpu() != 0, keep[0])
+
+
 # ---------------------------------------------------------------------- misc
 def test_colsum_and_tokens_and_head():
     o = ops()

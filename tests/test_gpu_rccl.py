@@ -1,0 +1,117 @@
+"""The DDP reducer on the real backend: a 1-rank "nccl" (= RCCL) process group on the test box's
+GPU (the driver's 1/2/4/8-GPU bench is the only multi-rank RCCL run; the reference itself is
+single-device, `/root/reference/train/train_image_vit.py:183`). Exercises fervit/ddp.py's nccl
+branch -- ReduceOp.AVG on the side stream, the bf16 wire casts, `work.wait` and the compute
+stream's join -- on a bf16 ViT with FusedAdamW: after 3 steps the wrapped model must equal an
+unwrapped twin bit for bit (fp32 wire: AVG over one rank is the identity) or equal it through the
+bf16 round trip of every gradient (bf16 wire), and bucket all-reduces must be issued while the
+backward is still running (overlap), not all at its end."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(port, wire, q):
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "fer-vit_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    import torch.distributed as dist
+
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    try:
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+        from fervit import ddp as D
+        from fervit import runtime
+        from fervit.loss import CrossEntropyLoss
+        from fervit.optim import FusedAdamW
+        from models_fer_vit.image_vit import ImageViT
+
+        def model():
+            torch.manual_seed(0)
+            m = ImageViT(img_size=48, patch_size=16, embed_dim=192, depth=3, heads=4, mlp_dim=384, dropout=0.0)
+            return m.to(dev).set_precision("bf16")
+
+        g = torch.Generator().manual_seed(5)
+        xs = [torch.randn(16, 3, 48, 48, generator=g).to(dev) for _ in range(3)]
+        ys = [torch.randint(0, 7, (16,), generator=g).to(dev) for _ in range(3)]
+        crit = CrossEntropyLoss(label_smoothing=0.1)
+        wire_dt = getattr(torch, wire)
+
+        ref = model()
+        ref_opt = FusedAdamW(ref.parameters(), lr=1e-3, weight_decay=0.05, model=ref)
+        m = model()
+        net = D.DistributedDataParallel(m, bucket_cap_mb=0.25, grad_dtype=wire_dt)
+        opt = FusedAdamW(m.parameters(), lr=1e-3, weight_decay=0.05, model=m)
+        events = []
+        orig_launch = D.Reducer._launch
+
+        def launch(self, b):
+            events.append(("launch", self.buckets.index(b)))
+            return orig_launch(self, b)
+
+        D.Reducer._launch = launch
+        runtime.register_grad_ready_hook(lambda ps: events.append(("ready", len(ps))))
+        grad_ok = []
+        for i in range(3):
+            ref_opt.zero_grad()
+            crit(ref(xs[i]), ys[i]).backward()
+            opt.zero_grad()
+            events.clear()
+            crit(net(xs[i]), ys[i]).backward()
+            torch.cuda.synchronize()
+            nb = len(net.reducer.buckets)
+            # every bucket launched, at least one while later layers' gradients were still coming
+            launched = [e for e in events if e[0] == "launch"]
+            last_ready = max(k for k, e in enumerate(events) if e[0] == "ready")
+            first_launch = min(k for k, e in enumerate(events) if e[0] == "launch")
+            overlap = first_launch < last_ready and len(launched) == nb
+            for p, r in zip(m.parameters(), ref.parameters()):
+                want = r.grad if wire == "float32" else r.grad.to(torch.bfloat16).float()
+                grad_ok.append(bool(torch.equal(p.grad, want)))
+            ref_opt.step()
+            opt.step()
+        torch.cuda.synchronize()
+        same = all(torch.equal(p, r) for p, r in zip(m.parameters(), ref.parameters()))
+        q.put(("ok", nb, overlap, all(grad_ok), same, dist.get_backend()))
+    except Exception as ex:  # noqa: BLE001
+        import traceback
+
+        q.put(("error", traceback.format_exc()[-2000:], str(ex)))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("wire", ["float32", "bfloat16"])
+def test_rccl_one_rank_reducer(wire):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_worker, args=(_port(), wire, q))
+    p.start()
+    res = q.get(timeout=180)
+    p.join(timeout=60)
+    assert res[0] == "ok", res[1]
+    _, nb, overlap, grads_equal, same, backend = res
+    assert backend == "nccl"
+    assert nb > 2, nb  # several buckets, so the overlap check means something
+    assert overlap
+    assert grads_equal
+    if wire == "float32":
+        assert same  # AVG over one rank is the identity: the replicas stay bit-identical

@@ -173,3 +173,122 @@ def test_layerwise_param_groups_cover_trainables():
     ids = {id(p) for g in groups for p in g["params"]}
     assert all(id(p) in ids for p in m.parameters() if p.requires_grad)
     assert [g["lr"] for g in groups][-1] == 5e-4 and groups[-1]["weight_decay"] == 0
+
+
+def _image_model(seed=0, dropout=0.1):
+    from models_fer_vit.image_vit import ImageViT
+
+    torch.manual_seed(seed)
+    m = ImageViT(img_size=48, patch_size=16, embed_dim=96, depth=2, heads=4, mlp_dim=192, dropout=dropout)
+    return m.to(DEV).set_precision("bf16")
+
+
+def test_reference_train_loop_bf16_with_torch_optimizer():
+    """The drop-in claim on the bf16 path: `train/train_image_vit.py`'s own loop
+    (train_epoch `:110-143`, torch.optim.AdamW(model.parameters()) `:270-276`, CosineAnnealingLR
+    stepped per epoch `:415-417`, torch.nn.utils.clip_grad_norm_, torch.use_deterministic_algorithms
+    (True) `:40`) runs unchanged on ImageViT. After every torch optimizer step the forward must read
+    the updated weights (the bf16 shadow follows the parameters' version counters): the model's eval
+    logits equal those of a fresh model built from its state_dict, bit for bit. The same loop with
+    FusedAdamW gives the same losses and parameters within bf16 tolerance."""
+    import fervit
+    from models_fer_vit.image_vit import ImageViT
+
+    loader = _loader(48, (3, 48, 48), 4, 16)
+    xe = torch.randn(8, 3, 48, 48, generator=torch.Generator().manual_seed(9)).to(DEV)
+    results = {}
+    prev = torch.are_deterministic_algorithms_enabled()
+    torch.use_deterministic_algorithms(True)
+    try:
+        for kind in ("torch", "fused"):
+            fervit.manual_seed(77)  # same dropout masks in both runs
+            m = _image_model(1)
+            crit = torch.nn.CrossEntropyLoss(label_smoothing=0.1)
+            if kind == "torch":
+                opt = torch.optim.AdamW(m.parameters(), lr=1e-3, weight_decay=0.05, betas=(0.9, 0.999))
+            else:
+                from fervit.optim import FusedAdamW
+
+                opt = FusedAdamW(m.parameters(), lr=1e-3, weight_decay=0.05, betas=(0.9, 0.999), model=m)
+            sched = torch.optim.lr_scheduler.CosineAnnealingLR(opt, T_max=3)
+            losses = []
+            for epoch in range(3):
+                m.train()
+                for images, labels in loader:
+                    images, labels = images.to(DEV), labels.to(DEV)
+                    opt.zero_grad()
+                    logits = m(images)
+                    loss = crit(logits, labels)
+                    loss.backward()
+                    torch.nn.utils.clip_grad_norm_(m.parameters(), 1.0)
+                    opt.step()
+                    losses.append(loss.item())
+                    if kind == "torch":
+                        # the forward reads the weights torch just wrote
+                        m.eval()
+                        with torch.no_grad():
+                            got = m(xe)
+                            twin = ImageViT(img_size=48, patch_size=16, embed_dim=96, depth=2, heads=4, mlp_dim=192,
+                                            dropout=0.1).to(DEV).set_precision("bf16")
+                            twin.load_state_dict(m.state_dict())
+                            twin.eval()
+                            assert torch.equal(got, twin(xe))
+                        m.train()
+                sched.step()
+            results[kind] = (losses, {k: v.detach().clone() for k, v in m.state_dict().items()})
+    finally:
+        torch.use_deterministic_algorithms(prev)
+    (l1, p1), (l2, p2) = results["torch"], results["fused"]
+    assert l1[-1] < l1[0]
+    for a, b in zip(l1, l2):
+        assert abs(a - b) < 2e-2 * max(1.0, abs(a))
+    for k in p1:
+        if p1[k].is_floating_point():
+            torch.testing.assert_close(p1[k], p2[k], rtol=0, atol=3e-3, msg=k)
+
+
+def test_clip_ignores_stale_grad_slots():
+    """fervit clip_grad_norm_ sums the flat gradient buffer: a parameter that got a gradient in
+    step 1 and none in step 2 (a stage frozen mid-run, then zero_grad(set_to_none=True)) must not
+    contribute its step-1 values -- the norm equals torch.nn.utils.clip_grad_norm_'s, which skips
+    `p.grad is None` (`train/train_latent_vit_v2.py:133`). Foreign `.grad` tensors count as torch
+    counts them."""
+    from fervit.loss import CrossEntropyLoss
+    from fervit.optim import FusedAdamW, clip_grad_norm_
+
+    m = _image_model(2, dropout=0.0)
+    crit = CrossEntropyLoss(label_smoothing=0.1)
+    o = FusedAdamW(m.parameters(), lr=1e-3, model=m)
+    g = torch.Generator().manual_seed(3)
+    x, y = torch.randn(8, 3, 48, 48, generator=g).to(DEV), torch.randint(0, 7, (8,), generator=g).to(DEV)
+    o.zero_grad()
+    crit(m(x), y).backward()
+    n_all = clip_grad_norm_(m, 1e9, optimizer=o)
+    torch.testing.assert_close(n_all, torch.nn.utils.clip_grad_norm_(m.parameters(), 1e9), rtol=1e-5, atol=0)
+    o.step()
+    # step 2: the patch embedding and the first layer are frozen (no gradient), the head gets a
+    # foreign gradient tensor assigned by user code
+    frozen = list(m.patch_embed.parameters()) + list(m.transformer.layers[0].parameters())
+    for p in frozen:
+        p.requires_grad_(False)
+    o.zero_grad(set_to_none=True)
+    crit(m(x), y).backward()
+    assert all(p.grad is None for p in frozen)
+    m.head.weight.grad = torch.full_like(m.head.weight, 0.25)
+    ours = clip_grad_norm_(m, 1e9, optimizer=o)
+    ref = torch.nn.utils.clip_grad_norm_(m.parameters(), 1e9)
+    torch.testing.assert_close(ours, ref, rtol=1e-5, atol=0)
+
+
+def test_zero_grad_drops_a_pending_clip_coefficient():
+    """A clip coefficient computed for a step that is then skipped must not scale the next step's
+    gradients: FusedAdamW.zero_grad clears it."""
+    from fervit.optim import FusedAdamW, clip_grad_norm_
+
+    m = _latent_model(6)
+    o = FusedAdamW(m.parameters(), lr=1e-3, model=m)
+    _set_grads(m, {id(p): torch.ones_like(p) * 10 for p in m.parameters()})
+    clip_grad_norm_(m, 1.0)
+    assert m._fer_clip_coef is not None
+    o.zero_grad()  # the step is skipped
+    assert m._fer_clip_coef is None and o.clip_coef is None
