@@ -207,15 +207,80 @@ FER_DEV void epi8_t(const EpiArgs& e, long m, long n, f32x4& v0, f32x4& v1, f32x
   }
 }
 
+// The fixed kinds with the row addressing done by the caller (element offsets oc / op into c / pre
+// and the dropout index di, advanced by adds per row instead of a 64-bit multiply per store) and
+// the dropout scale folded into constants: GATE takes it in the GELU constants (gelu_and_grad8s),
+// RES as acc * (alpha*s) + b*s (ab = alpha*s, b0 / b1 pre-scaled by the caller), so a dropped
+// element costs a select only.
+template <int S0>
+FER_DEV void epi8_k(const EpiArgs& e, long oc, long op, uint32_t di, f32x4& v0, f32x4& v1, f32x4 b0, f32x4 b1,
+                    bf16x8 x, uint64_t seed, float ab, f32x2 ghs, f32x2 gps) {
+  constexpr int S = epi_base(S0);
+  static_assert(S != EPI_GEN, "generic epilogue goes through epi8_t");
+  v0 = v0 * ab + b0;
+  v1 = v1 * ab + b1;
+  if constexpr (S == EPI_GATE) {
+    f32x4 g0, g1;
+    f32x2 xs[4] = {v0.xy, v0.zw, v1.xy, v1.zw}, gs[4];
+    gelu_and_grad8s(xs, gs, ghs, gps);
+    v0.xy = xs[0]; v0.zw = xs[1]; v1.xy = xs[2]; v1.zw = xs[3];
+    g0.xy = gs[0]; g0.zw = gs[1]; g1.xy = gs[2]; g1.zw = gs[3];
+    if (e.drop_thresh) {
+      bool kp[8];
+      keep8(seed, di, e.drop_thresh, kp);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        v0[r] = kp[r] ? v0[r] : 0.f;
+        v1[r] = kp[4 + r] ? v1[r] : 0.f;
+        g0[r] = kp[r] ? g0[r] : 0.f;
+        g1[r] = kp[4 + r] ? g1[r] : 0.f;
+      }
+    }
+#ifdef FER_GEMM_EXP
+    if (e.colsum_accumulate & 0x100) {
+      const bf16x8 pg = pack8(g0, g1);
+      asm volatile("" ::"v"(pg));
+    } else
+#endif
+    *(bf16x8*)((bf16*)e.pre + op) = pack8(g0, g1);
+  }
+  if constexpr (S == EPI_RES) {
+    if (e.drop_thresh) {
+      bool kp[8];
+      keep8(seed, di, e.drop_thresh, kp);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        v0[r] = kp[r] ? v0[r] : 0.f;
+        v1[r] = kp[4 + r] ? v1[r] : 0.f;
+      }
+    }
+    v0 += lo4(x);
+    v1 += hi4(x);
+  }
+  if constexpr (S == EPI_MUL) {
+    v0 *= lo4(x);
+    v1 *= hi4(x);
+  }
+#ifdef FER_GEMM_EXP
+  if (e.colsum_accumulate & 0x100) {  // experiments library only: no output store (values kept live)
+    const bf16x8 pv = pack8(v0, v1);
+    asm volatile("" ::"v"(pv));
+    return;
+  }
+#endif
+  *(bf16x8*)((bf16*)e.c + oc) = pack8(v0, v1);
+}
+
 // kind for a launch (EPI_GEN unless every flag matches one of the fixed kinds)
 static inline int epi_kind(const EpiArgs& e) {
   if (e.c_f32 || e.accumulate || e.post_scale) return EPI_GEN;
   const int act = e.act & 15;
   const bool gate = (e.act & FER_PRE_GATE) && e.pre;
-  if (gate) return (act == FER_ACT_GELU && !e.aux && !e.res) ? EPI_GATE : EPI_GEN;
+  if (gate) return (act == FER_ACT_GELU && !e.aux && !e.res && !e.colsum) ? EPI_GATE : EPI_GEN;
   if (e.pre || act) return EPI_GEN;
   static const bool xdma = getenv("FERVIT_EPI_XDMA") != nullptr;  // A/B: row operand through LDS-DMA
   if (e.aux) return (e.aux_act == FER_ACT_MUL && !e.res && !e.drop_thresh) ? (xdma ? EPI_MUL : EPI_MUL2) : EPI_GEN;
+  if (e.colsum) return EPI_GEN;
   if (e.res) return xdma ? EPI_RES : EPI_RES2;
   return e.drop_thresh ? EPI_GEN : EPI_STORE;
 }
@@ -493,6 +558,16 @@ FER_DEV void tile_epilogue(const GemmArgs& g, const EpiArgs& e, AccT (&acc)[FN][
   }
   const float ps = e.post_scale ? *e.post_scale : 1.f;
   const uint64_t seed = e.drop_thresh ? step_seed(e.seed) : 0;
+  // fixed kinds (epi8_k): dropout scale folded into the bias / alpha (RES) or the GELU constants (GATE)
+  constexpr bool KIND = EK != EPI_GEN;
+  constexpr bool CS = !KIND || epi_base(EK) == EPI_MUL;  // only these kinds carry fused column sums
+  const float dsc = e.drop_thresh ? e.drop_scale : 1.f;
+  const float ab = epi_base(EK) == EPI_RES ? e.alpha * dsc : e.alpha;
+  if constexpr (epi_base(EK) == EPI_RES) {
+    b0 *= dsc;
+    b1 *= dsc;
+  }
+  const f32x2 ghs = f32x2(0.5f * dsc), gps = f32x2(0.39894228040143268f * dsc);  // GATE: gelu_and_grad8s
   const void* xs = e.res ? e.res : e.aux;  // the row operand brought in by DMA
   const long ldxs = e.res ? e.ldr : e.ldx;
   const __amdgpu_buffer_rsrc_t rx = make_rsrc(xs);
@@ -548,6 +623,9 @@ FER_DEV void tile_epilogue(const GemmArgs& g, const EpiArgs& e, AccT (&acc)[FN][
   f32x4 cs0 = f32x4{0.f, 0.f, 0.f, 0.f}, cs1 = cs0;  // fused column sums of this thread's rows
   auto finish = [&](int h, const char* stg) {
     const char* xh = xb + (h & 1) * XBYTES;
+    const long mr = m0 + h * EROWS + tr;  // this thread's first row of the chunk
+    long oc = mr * e.ldc + n, op = mr * e.ldp + n;
+    uint32_t di = (uint32_t)mr * (uint32_t)e.drop_ld + (uint32_t)n;
 #pragma unroll 1
     for (int it = 0; it < IT; ++it) {
       const int r = tr + it * RPI;
@@ -555,10 +633,16 @@ FER_DEV void tile_epilogue(const GemmArgs& g, const EpiArgs& e, AccT (&acc)[FN][
       f32x4 v0 = *(const f32x4*)(stg + swz(r, tc)), v1 = *(const f32x4*)(stg + swz(r, tc + 4));
       const bf16x8 x = xs ? *(const bf16x8*)(xh + (r * BN + tc) * 2) : bf16x8{};
       if (nok && m < g.M) {
-        epi8_t<EK>(e, m, n, v0, v1, b0, b1, x, ps, seed);
-        cs0 += v0;
-        cs1 += v1;
+        if constexpr (KIND) epi8_k<EK>(e, oc, op, di, v0, v1, b0, b1, x, seed, ab, ghs, gps);
+        else epi8_t<EK>(e, m, n, v0, v1, b0, b1, x, ps, seed);
+        if constexpr (CS) {
+          cs0 += v0;
+          cs1 += v1;
+        }
       }
+      oc += RPI * e.ldc;
+      op += RPI * e.ldp;
+      di += (uint32_t)RPI * (uint32_t)e.drop_ld;
     }
   };
   if constexpr ((EK == EPI_RES2 || EK == EPI_MUL2) && EPC == 2 && 2 * EROWS * SROW <= SMEMB) {
@@ -575,6 +659,9 @@ FER_DEV void tile_epilogue(const GemmArgs& g, const EpiArgs& e, AccT (&acc)[FN][
     };
     auto finish_x = [&](int h, const char* stg, const bf16x8* xr) {
       f32x4 v0 = *(const f32x4*)(stg + swz(tr, tc)), v1 = *(const f32x4*)(stg + swz(tr, tc + 4));
+      const long mr = m0 + h * EROWS + tr;
+      const long oc0 = mr * e.ldc + n;
+      const uint32_t di0 = (uint32_t)mr * (uint32_t)e.drop_ld + (uint32_t)n;
 #pragma unroll
       for (int it = 0; it < IT; ++it) {
         const int r = tr + it * RPI;
@@ -585,9 +672,12 @@ FER_DEV void tile_epilogue(const GemmArgs& g, const EpiArgs& e, AccT (&acc)[FN][
           n1 = *(const f32x4*)(stg + swz(r + RPI, tc + 4));
         }
         if (nok && m < g.M) {
-          epi8_t<EK>(e, m, n, v0, v1, b0, b1, xr[it], ps, seed);
-          cs0 += v0;
-          cs1 += v1;
+          epi8_k<EK>(e, oc0 + (long)it * RPI * e.ldc, 0, di0 + (uint32_t)(it * RPI) * (uint32_t)e.drop_ld, v0, v1,
+                     b0, b1, xr[it], seed, ab, ghs, gps);
+          if constexpr (CS) {
+            cs0 += v0;
+            cs1 += v1;
+          }
         }
         v0 = n0;
         v1 = n1;
@@ -711,8 +801,11 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g, 
   const int wm = wave % WM, wn = wave / WM;
 
   int tm, tn, ks = 0;
-  if (gridDim.y > 1) split_tile_of(g.tiles_m, g.tiles_n, tm, tn, ks);
-  else tile_of(blockIdx.x, g.tiles_m, g.tiles_n, tm, tn);
+  if (gridDim.y > 1 && !(g.dbg & 16)) split_tile_of(g.tiles_m, g.tiles_n, tm, tn, ks);  // dbg 16: A/B
+  else {
+    tile_of(blockIdx.x, g.tiles_m, g.tiles_n, tm, tn);
+    ks = blockIdx.y;
+  }
   const int m0 = tm * BM, n0 = tn * BN;
   const int kbeg = ks * g.k_chunk;
   const int kend = min(g.K, kbeg + g.k_chunk);
@@ -818,8 +911,11 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_ring_kernel(GemmArgs g, 
   const int wm = wave % WM, wn = wave / WM;
 
   int tm, tn, ks = 0;
-  if (gridDim.y > 1) split_tile_of(g.tiles_m, g.tiles_n, tm, tn, ks);
-  else tile_of(blockIdx.x, g.tiles_m, g.tiles_n, tm, tn);
+  if (gridDim.y > 1 && !(g.dbg & 16)) split_tile_of(g.tiles_m, g.tiles_n, tm, tn, ks);  // dbg 16: A/B
+  else {
+    tile_of(blockIdx.x, g.tiles_m, g.tiles_n, tm, tn);
+    ks = blockIdx.y;
+  }
   const int m0 = tm * BM, n0 = tn * BN;
   const int kbeg = ks * g.k_chunk;
   const int kend = min(g.K, kbeg + g.k_chunk);
@@ -936,8 +1032,11 @@ __global__ __launch_bounds__(256, 2) void gemm_pp_kernel(GemmArgs g, EpiArgs e) 
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave % WM, wn = wave / WM;
   int tm, tn, ks = 0;
-  if (gridDim.y > 1) split_tile_of(g.tiles_m, g.tiles_n, tm, tn, ks);
-  else tile_of(blockIdx.x, g.tiles_m, g.tiles_n, tm, tn);
+  if (gridDim.y > 1 && !(g.dbg & 16)) split_tile_of(g.tiles_m, g.tiles_n, tm, tn, ks);  // dbg 16: A/B
+  else {
+    tile_of(blockIdx.x, g.tiles_m, g.tiles_n, tm, tn);
+    ks = blockIdx.y;
+  }
   const int m0 = tm * BM, n0 = tn * BN;
   const int kbeg = ks * g.k_chunk;
   const int kend = min(g.K, kbeg + g.k_chunk);
@@ -1248,6 +1347,14 @@ template <bool AKC, bool BKC, int MT, bool DYN, int EK>
 __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmArgs g, EpiArgs e) {
   __shared__ __attribute__((aligned(1024))) char smem[8 * 16384 + 16];
   const int ntiles = g.tiles_m * g.tiles_n;
+#ifdef FER_GEMM_EXP
+  // experiments library only (dbg & 64): workgroups with an odd (blockIdx.x / 8) start (dbg >> 8) k
+  // cycles late, so that the two halves of every XCD reach their tile epilogues at different times
+  if ((g.dbg & 64) && ((blockIdx.x >> 3) & 1)) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    while (__builtin_amdgcn_s_memtime() - t0 < (unsigned long long)(g.dbg >> 8) * 1024ull) __builtin_amdgcn_s_sleep(8);
+  }
+#endif
   if constexpr (!DYN) {
 #pragma unroll 1
     for (int bid = blockIdx.x; bid < ntiles; bid += gridDim.x) {
@@ -1463,6 +1570,9 @@ int gemm_launch(const GemmDesc& d, const EpiArgs& e_in, hipStream_t st) {
   g.M = d.M; g.N = d.N; g.K = d.K;
   static const int dbg = getenv("FERVIT_GEMM_DBG") ? atoi(getenv("FERVIT_GEMM_DBG")) : 0;
   g.dbg = dbg;
+#ifdef FER_GEMM_EXP
+  if (dbg & 32) e.colsum_accumulate |= 0x100;  // experiments library: epilogue without output stores
+#endif
   if (d.M <= 0 || d.N <= 0) return 0;
   if (d.N % 4) return set_error("gemm: N must be a multiple of 4");
   if (e.colsum && (!d.ws || d.ws_bytes < fer_gemm_colsum_ws(d.M, d.N)))
