@@ -490,7 +490,11 @@ __device__ unsigned long long g_epst[2][16];
 #define EP_STAMP(i) do {} while (0)
 #endif
 
-// ---- epilogue. Accumulator element (i, j, q, r) -> tile row/col. Split-K partials go to
+// ---- epilogue. Every workgroup barrier in the epilogue (and between the tiles of a persistent
+// workgroup) is bar_lds (lgkmcnt(0) + s_barrier): the barriers order LDS staging only. (With no
+// LDS-DMA in flight hipcc lowers __syncthreads to the same two instructions; bar_lds makes sure no
+// vmcnt(0) -- a wait for every earlier output store -- can appear there.)
+// Accumulator element (i, j, q, r) -> tile row/col. Split-K partials go to
 // the fp32 slab; otherwise each wave-row half of the tile (in EPC row chunks) is staged
 // through LDS as fp32 with padded rows and every thread applies the epilogue on 4 consecutive
 // columns of one row: all global traffic of the epilogue is row-contiguous.
@@ -599,7 +603,7 @@ FER_DEV void tile_epilogue(const GemmArgs& g, const EpiArgs& e, AccT (&acc)[FN][
     }
   };
   auto stage = [&](int h, int half, int sub) {
-    __syncthreads();  // every wave is done with the staging area and with X[(h+1)&1]
+    bar_lds();  // every wave is done with the staging area and with X[(h+1)&1]
     const bool more = h + 1 < 2 * EPC;
     if (xs && more) issue_x(h + 1);
     if (wm == half) {
@@ -618,7 +622,7 @@ FER_DEV void tile_epilogue(const GemmArgs& g, const EpiArgs& e, AccT (&acc)[FN][
       const int after = (more ? PPW : 0) + (h > 0 ? spc : 0);
       wait_x(spc < 0 ? 0 : after);
     }
-    __syncthreads();  // staging and X[h&1] (all waves' DMA) visible
+    bar_lds();  // staging and X[h&1] (all waves' DMA) visible
   };
   f32x4 cs0 = f32x4{0.f, 0.f, 0.f, 0.f}, cs1 = cs0;  // fused column sums of this thread's rows
   auto finish = [&](int h, const char* stg) {
@@ -697,18 +701,18 @@ FER_DEV void tile_epilogue(const GemmArgs& g, const EpiArgs& e, AccT (&acc)[FN][
     };
     bf16x8 xr[2 * IT];
     load_x(0, xr);
-    __syncthreads();
+    bar_lds();
     put(std::integral_constant<int, 0>{});
-    __syncthreads();
+    bar_lds();
     EP_STAMP(1);
     finish_x(0, stg, xr);
     EP_STAMP(2);
     finish_x(EPC, stg + EROWS * SROW, xr + IT);
     EP_STAMP(3);
     load_x(1, xr);
-    __syncthreads();
+    bar_lds();
     put(std::integral_constant<int, 1>{});
-    __syncthreads();
+    bar_lds();
     EP_STAMP(5);
     finish_x(1, stg, xr);
     EP_STAMP(6);
@@ -722,7 +726,7 @@ FER_DEV void tile_epilogue(const GemmArgs& g, const EpiArgs& e, AccT (&acc)[FN][
     // half w is tile chunk h = 2w + p (rows 64h..64h+63)
 #pragma unroll 1
     for (int p = 0; p < EPC; ++p) {
-      __syncthreads();  // every wave is done with both staging areas
+      bar_lds();  // every wave is done with both staging areas
       // accumulator indices must be compile-time constants (a run-time p would index the
       // accumulator array dynamically: scratch)
       auto put = [&](auto sub) {
@@ -739,7 +743,7 @@ FER_DEV void tile_epilogue(const GemmArgs& g, const EpiArgs& e, AccT (&acc)[FN][
       };
       if (p == 0) put(std::integral_constant<int, 0>{});
       else put(std::integral_constant<int, 1>{});
-      __syncthreads();
+      bar_lds();
       EP_STAMP(1 + 4 * p);
       finish(p, stg);
       EP_STAMP(2 + 4 * p);
@@ -763,11 +767,11 @@ FER_DEV void tile_epilogue(const GemmArgs& g, const EpiArgs& e, AccT (&acc)[FN][
     }
   }
   if (g.cs_part) {  // column partial sums of this tile -> cs_part[tile row][n], fixed order
-    __syncthreads();  // staging area free
+    bar_lds();  // staging area free
     float* red = (float*)smem;  // [RPI][BN]
     *(f32x4*)(red + tr * BN + tc) = cs0;
     *(f32x4*)(red + tr * BN + tc + 4) = cs1;
-    __syncthreads();
+    bar_lds();
     for (int c = tid_; c < BN; c += NT) {
       float t = 0.f;
       for (int r = 0; r < RPI; ++r) t += red[r * BN + c];
@@ -1081,7 +1085,7 @@ __global__ __launch_bounds__(256, 2) void gemm_pp_kernel(GemmArgs g, EpiArgs e) 
 #pragma unroll
       for (int i = 0; i < FN; ++i) acc[i][j] = mfma<MT>(bfr[i], af[j], acc[i][j]);
   }
-  __syncthreads();  // every wave's fragment reads are done: the ring becomes epilogue staging
+  bar_lds();  // every wave's fragment reads are done: the ring becomes epilogue staging
   tile_epilogue<BM, BN, WM, WN, MT, 2, NST * STAGE, EK>(g, e, acc, smem, m0, n0, ks, wm, wn, lane);
 }
 
@@ -1359,7 +1363,7 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmArgs g, EpiArgs e)
 #pragma unroll 1
     for (int bid = blockIdx.x; bid < ntiles; bid += gridDim.x) {
       tile_8ph<AKC, BKC, MT, EK>(g, e, bid, smem, nullptr);
-      __syncthreads();  // every wave is done with the epilogue's LDS before the next tile's DMA
+      bar_lds();  // every wave is done with the epilogue's LDS before the next tile's DMA
     }
   } else {
     volatile int* slot = (volatile int*)(smem + 8 * 16384);
@@ -1367,7 +1371,7 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmArgs g, EpiArgs e)
 #pragma unroll 1
     while (bid >= 0) {
       tile_8ph<AKC, BKC, MT, EK>(g, e, bid, smem, slot + par);
-      __syncthreads();  // every wave is done with the epilogue's LDS before the next tile's DMA
+      bar_lds();  // every wave is done with the epilogue's LDS before the next tile's DMA
       bid = __builtin_amdgcn_readfirstlane(slot[par]);
       par ^= 1;
     }

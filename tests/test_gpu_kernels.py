@@ -392,7 +392,11 @@ def test_attention_persistent_multi_unit(N, H, dh, B, p):
         for j, name in enumerate("qkv"):
             assert rel_err(dqkv[:, j * D:(j + 1) * D], qr.grad[:, j * D:(j + 1) * D]) < 4e-2, (mode, name)
         assert rel_err(cs, qr.grad.sum(0)) < 4e-2, mode
-        results.append((out, saved, dqkv, cs))
+        # the saved state's alignment padding is never written: compare lse and the keep words only
+        nw = B * H * ((N + 31) // 32) ** 2 * 32 if p > 0 else 0
+        off = (B * H * N + 63) // 64 * 64
+        # (the keep words compared as integers: as floats most of them are NaN bit patterns)
+        results.append((out, saved[:B * H * N], saved[off:off + nw].view(torch.int32), dqkv, cs))
     for a, b in zip(*results):
         assert torch.equal(a, b)
 

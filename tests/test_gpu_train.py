@@ -243,8 +243,16 @@ def test_reference_train_loop_bf16_with_torch_optimizer():
     for a, b in zip(l1, l2):
         assert abs(a - b) < 2e-2 * max(1.0, abs(a))
     for k in p1:
-        if p1[k].is_floating_point():
-            torch.testing.assert_close(p1[k], p2[k], rtol=0, atol=3e-3, msg=k)
+        if not p1[k].is_floating_point():
+            continue
+        a, b = p1[k], p2[k]
+        if k.endswith("in_proj_bias"):
+            # the key third has an exactly-zero true gradient (softmax is invariant to it): its
+            # rounding noise differs between the two optimizers and Adam turns it into +-lr steps
+            D = a.numel() // 3
+            assert (a[D:2 * D] - b[D:2 * D]).abs().max().item() <= 2 * len(l1) * 1e-3 + 1e-6, k
+            a, b = torch.cat([a[:D], a[2 * D:]]), torch.cat([b[:D], b[2 * D:]])
+        torch.testing.assert_close(a, b, rtol=0, atol=3e-3, msg=k)
 
 
 def test_clip_ignores_stale_grad_slots():
