@@ -270,7 +270,7 @@ FER_DEV void fwd_load_q(bf16x8 (&qf)[4], const bf16* qkv, long ldq, int unit, in
   }
 }
 
-template <int NB, bool PIPE = true>
+template <int NB>
 __global__ __launch_bounds__(64 * (NB + 1)) void attn_fwd_pers(const bf16* __restrict__ qkv, long ldq,
                                                                bf16* __restrict__ out, long ldo,
                                                                float* __restrict__ lse, uint32_t* __restrict__ mask,
@@ -387,32 +387,6 @@ __global__ __launch_bounds__(64 * (NB + 1)) void attn_fwd_pers(const bf16* __res
           for (int db = 0; db < 2; ++db) ot[db] = mfma32(vfr[s2][db], pf, ot[db]);
         }
       };
-      if constexpr (PIPE) {
-        // software pipeline (cdna guide T15): S^T of key block kb+1 is issued to the matrix pipe
-        // before the softmax of block kb, which hides it; the K fragments run one block further
-        // ahead. Fully unrolled, so the two S^T buffers are named registers.
-        f32x16 sb[2];
-        sb[0] = f32x16{};
-#pragma unroll
-        for (int s = 0; s < 4; ++s) sb[0] = mfma32(kfr[s], qf[s], sb[0]);
-        if (NB > 1) {
-#pragma unroll
-          for (int s = 0; s < 4; ++s) kfr[s] = rd_row(Ki, 32 + (lane & 31), 2 * s + hh);
-        }
-#pragma unroll
-        for (int kb = 0; kb < NB; ++kb) {
-          if (kb + 1 < NB) {
-            sb[(kb + 1) & 1] = f32x16{};
-#pragma unroll
-            for (int s = 0; s < 4; ++s) sb[(kb + 1) & 1] = mfma32(kfr[s], qf[s], sb[(kb + 1) & 1]);
-            if (kb + 2 < NB) {
-#pragma unroll
-              for (int s = 0; s < 4; ++s) kfr[s] = rd_row(Ki, (kb + 2) * 32 + (lane & 31), 2 * s + hh);
-            }
-          }
-          block(kb, sb[kb & 1]);
-        }
-      } else {
 #pragma unroll 1
         for (int kb = 0; kb < NB; ++kb) {
           f32x16 st = {};
@@ -424,7 +398,6 @@ __global__ __launch_bounds__(64 * (NB + 1)) void attn_fwd_pers(const bf16* __res
           }
           block(kb, st);
         }
-      }
       l = xhalf_sum(l);
       if (q < N) {
         store_rows_q(out + ((long)b * N + q) * ldo + h * dh, ot[0], ot[1], dscale / l, hh, dh);
@@ -1561,17 +1534,11 @@ extern "C" int fer_attention_fwd(int dtype, const void* qkv, int64_t ld_qkv, voi
     uint32_t* mask = (drop_thresh && pers_path(dtype, N, dh)) ? (uint32_t*)(lse + lse_floats(B, N, H)) : nullptr;
     const int grid = std::min(B * H, n_cus());
     const WqArgs wq = fixed_stride() ? WqArgs{} : wq_prepare_here(st, grid, B * H);
-    static const bool nopipe = getenv("FERVIT_ATTN_FWD_NOPIPE") != nullptr;  // A/B switch
 #define FER_FPERS(NBV)                                                                                       \
   case NBV:                                                                                                  \
-    if (nopipe)                                                                                              \
-      hipLaunchKernelGGL((attn_fwd_pers<NBV, false>), dim3(grid), dim3(64 * (NBV + 1)), 0, st,               \
-                         (const bf16*)qkv, (long)ld_qkv, (bf16*)out, (long)ld_out, lse, mask, B * H, N, H, dh, \
-                         sl2, drop_thresh, drop_scale, seed, wq);                                           \
-    else                                                                                                     \
-      hipLaunchKernelGGL((attn_fwd_pers<NBV, true>), dim3(grid), dim3(64 * (NBV + 1)), 0, st,                \
-                         (const bf16*)qkv, (long)ld_qkv, (bf16*)out, (long)ld_out, lse, mask, B * H, N, H, dh, \
-                         sl2, drop_thresh, drop_scale, seed, wq);                                           \
+    hipLaunchKernelGGL(attn_fwd_pers<NBV>, dim3(grid), dim3(64 * (NBV + 1)), 0, st, (const bf16*)qkv,        \
+                       (long)ld_qkv, (bf16*)out, (long)ld_out, lse, mask, B * H, N, H, dh, sl2, drop_thresh,  \
+                       drop_scale, seed, wq);                                                               \
     break;
     switch (nb) {
       FER_FPERS(1) FER_FPERS(2) FER_FPERS(3) FER_FPERS(4) FER_FPERS(5) FER_FPERS(6) FER_FPERS(7)

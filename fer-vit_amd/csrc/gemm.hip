@@ -134,9 +134,10 @@ FER_DEV void epi8_bf16(const EpiArgs& e, long m, long n, f32x4& v0, f32x4& v1, f
 // generic epi8_bf16 tests every flag per row piece, and its branches and the register shuffles
 // between them cost more issue slots than the arithmetic of the plain and residual epilogues.
 // Same operations in the same order as epi8_bf16, so the results are bit-identical.
-enum { EPI_GEN = 0, EPI_STORE = 1, EPI_GATE = 2, EPI_RES = 3, EPI_MUL = 4, EPI_RES2 = 5, EPI_MUL2 = 6 };
+enum { EPI_GEN = 0, EPI_STORE = 1, EPI_GATE = 2, EPI_RES = 3, EPI_MUL = 4, EPI_RES2 = 5, EPI_MUL2 = 6, EPI_GATER = 7 };
 //   EPI_STORE: c = alpha*acc + bias                                   (qkv fwd, out-proj dgrad)
 //   EPI_GATE : c = drop(gelu(v)), pre = drop(gelu'(v)), v = alpha*acc + bias      (fc1 fwd)
+//   EPI_GATER: c = drop(relu(v)), pre = drop(v > 0)              (fc1 fwd of the ReLU encoders)
 //   EPI_RES  : c = drop(alpha*acc + bias) + res                (out-proj / fc2 fwd, dgrad + res)
 //   EPI_MUL  : c = (alpha*acc + bias) * aux                      (fc2 dgrad through the gate)
 // (bf16 c without accumulate, no post_scale; dropout is a run-time choice in GATE and RES)
@@ -214,11 +215,31 @@ FER_DEV void epi8_t(const EpiArgs& e, long m, long n, f32x4& v0, f32x4& v1, f32x
 // element costs a select only.
 template <int S0>
 FER_DEV void epi8_k(const EpiArgs& e, long oc, long op, uint32_t di, f32x4& v0, f32x4& v1, f32x4 b0, f32x4 b1,
-                    bf16x8 x, uint64_t seed, float ab, f32x2 ghs, f32x2 gps) {
+                    bf16x8 x, uint64_t seed, float ab, f32x2 ghs, f32x2 gps, float dsr) {
   constexpr int S = epi_base(S0);
   static_assert(S != EPI_GEN, "generic epilogue goes through epi8_t");
   v0 = v0 * ab + b0;
   v1 = v1 * ab + b1;
+  if constexpr (S == EPI_GATER) {  // scale folded into ab / b (relu(x) * s = relu(x * s), s > 0)
+    f32x4 g0, g1;
+    bool kp[8];
+    if (e.drop_thresh) keep8(seed, di, e.drop_thresh, kp);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const bool k0 = e.drop_thresh ? kp[r] : true, k1 = e.drop_thresh ? kp[4 + r] : true;
+      g0[r] = (k0 && v0[r] > 0.f) ? dsr : 0.f;
+      g1[r] = (k1 && v1[r] > 0.f) ? dsr : 0.f;
+      v0[r] = k0 ? fmaxf(v0[r], 0.f) : 0.f;
+      v1[r] = k1 ? fmaxf(v1[r], 0.f) : 0.f;
+    }
+#ifdef FER_GEMM_EXP
+    if (e.colsum_accumulate & 0x100) {
+      const bf16x8 pg = pack8(g0, g1);
+      asm volatile("" ::"v"(pg));
+    } else
+#endif
+    *(bf16x8*)((bf16*)e.pre + op) = pack8(g0, g1);
+  }
   if constexpr (S == EPI_GATE) {
     f32x4 g0, g1;
     f32x2 xs[4] = {v0.xy, v0.zw, v1.xy, v1.zw}, gs[4];
@@ -276,7 +297,10 @@ static inline int epi_kind(const EpiArgs& e) {
   if (e.c_f32 || e.accumulate || e.post_scale) return EPI_GEN;
   const int act = e.act & 15;
   const bool gate = (e.act & FER_PRE_GATE) && e.pre;
-  if (gate) return (act == FER_ACT_GELU && !e.aux && !e.res && !e.colsum) ? EPI_GATE : EPI_GEN;
+  if (gate) {
+    if (e.aux || e.res || e.colsum) return EPI_GEN;
+    return act == FER_ACT_GELU ? EPI_GATE : (act == FER_ACT_RELU ? EPI_GATER : EPI_GEN);
+  }
   if (e.pre || act) return EPI_GEN;
   static const bool xdma = getenv("FERVIT_EPI_XDMA") != nullptr;  // A/B: row operand through LDS-DMA
   if (e.aux) return (e.aux_act == FER_ACT_MUL && !e.res && !e.drop_thresh) ? (xdma ? EPI_MUL : EPI_MUL2) : EPI_GEN;
@@ -566,8 +590,8 @@ FER_DEV void tile_epilogue(const GemmArgs& g, const EpiArgs& e, AccT (&acc)[FN][
   constexpr bool KIND = EK != EPI_GEN;
   constexpr bool CS = !KIND || epi_base(EK) == EPI_MUL;  // only these kinds carry fused column sums
   const float dsc = e.drop_thresh ? e.drop_scale : 1.f;
-  const float ab = epi_base(EK) == EPI_RES ? e.alpha * dsc : e.alpha;
-  if constexpr (epi_base(EK) == EPI_RES) {
+  const float ab = (epi_base(EK) == EPI_RES || EK == EPI_GATER) ? e.alpha * dsc : e.alpha;
+  if constexpr (epi_base(EK) == EPI_RES || EK == EPI_GATER) {
     b0 *= dsc;
     b1 *= dsc;
   }
@@ -637,7 +661,7 @@ FER_DEV void tile_epilogue(const GemmArgs& g, const EpiArgs& e, AccT (&acc)[FN][
       f32x4 v0 = *(const f32x4*)(stg + swz(r, tc)), v1 = *(const f32x4*)(stg + swz(r, tc + 4));
       const bf16x8 x = xs ? *(const bf16x8*)(xh + (r * BN + tc) * 2) : bf16x8{};
       if (nok && m < g.M) {
-        if constexpr (KIND) epi8_k<EK>(e, oc, op, di, v0, v1, b0, b1, x, seed, ab, ghs, gps);
+        if constexpr (KIND) epi8_k<EK>(e, oc, op, di, v0, v1, b0, b1, x, seed, ab, ghs, gps, dsc);
         else epi8_t<EK>(e, m, n, v0, v1, b0, b1, x, ps, seed);
         if constexpr (CS) {
           cs0 += v0;
@@ -677,7 +701,7 @@ FER_DEV void tile_epilogue(const GemmArgs& g, const EpiArgs& e, AccT (&acc)[FN][
         }
         if (nok && m < g.M) {
           epi8_k<EK>(e, oc0 + (long)it * RPI * e.ldc, 0, di0 + (uint32_t)(it * RPI) * (uint32_t)e.drop_ld, v0, v1,
-                     b0, b1, xr[it], seed, ab, ghs, gps);
+                     b0, b1, xr[it], seed, ab, ghs, gps, dsc);
           if constexpr (CS) {
             cs0 += v0;
             cs1 += v1;
@@ -720,7 +744,8 @@ FER_DEV void tile_epilogue(const GemmArgs& g, const EpiArgs& e, AccT (&acc)[FN][
     EP_STAMP(7);
     EP_STAMP(4);
     EP_STAMP(8);
-  } else if constexpr ((EK == EPI_STORE || EK == EPI_GATE) && EPC == 2 && 2 * EROWS * SROW <= SMEMB) {
+  } else if constexpr ((EK == EPI_STORE || EK == EPI_GATE || EK == EPI_GATER) && EPC == 2 &&
+                       2 * EROWS * SROW <= SMEMB) {
     // no row operand: the X buffers' LDS holds a second staging area, so both wave-row halves
     // stage a chunk at once (all waves write, two barrier rounds instead of four); chunk sub p of
     // half w is tile chunk h = 2w + p (rows 64h..64h+63)
@@ -1028,6 +1053,15 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_ring_kernel(GemmArgs g, 
 template <bool AKC, bool BKC, int EK = EPI_GEN>
 __global__ __launch_bounds__(256, 2) void gemm_pp_kernel(GemmArgs g, EpiArgs e) {
   typedef f32x4 AccT;
+#ifdef FER_GEMM_EXP
+  // experiments library only: start one of the two workgroups of a CU (dbg 64: blocks 256..511 of the
+  // first dispatch round; dbg 128: odd blocks of it) (dbg >> 8) k cycles late, so that the pair runs
+  // its main loops and epilogues out of phase; the slot keeps that offset for its later blocks
+  if (blockIdx.x < 512 && (((g.dbg & 64) && blockIdx.x >= 256) || ((g.dbg & 128) && (blockIdx.x & 1)))) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    while (__builtin_amdgcn_s_memtime() - t0 < (unsigned long long)(g.dbg >> 8) * 1024ull) __builtin_amdgcn_s_sleep(8);
+  }
+#endif
   constexpr int BM = 256, BN = 128, WM = 2, WN = 2, MT = 16, RBK = 32, NST = 3, NW = 4;
   constexpr int TM = BM / WM, TN = BN / WN, FM = TM / MT, FN = TN / MT;
   constexpr int A_BYTES = BM * RBK * 2, B_BYTES = BN * RBK * 2, STAGE = A_BYTES + B_BYTES;
@@ -1102,6 +1136,7 @@ static int launch_pp(GemmArgs g, const EpiArgs& e, hipStream_t st) {
     switch (ek) {
       case EPI_STORE: FER_PPK(EPI_STORE); break;
       case EPI_GATE: FER_PPK(EPI_GATE); break;
+      case EPI_GATER: FER_PPK(EPI_GATER); break;
       case EPI_RES: FER_PPK(EPI_RES); break;
       case EPI_MUL: FER_PPK(EPI_MUL); break;
       case EPI_RES2: FER_PPK(EPI_RES2); break;
@@ -1454,6 +1489,7 @@ static int launch_bf16(GemmArgs g, const EpiArgs& e, hipStream_t st) {
     switch (ek) {
       case EPI_STORE: FER_BF16K(EPI_STORE); break;
       case EPI_GATE: FER_BF16K(EPI_GATE); break;
+      case EPI_GATER: FER_BF16K(EPI_GATER); break;
       case EPI_RES: FER_BF16K(EPI_RES); break;
       case EPI_MUL: FER_BF16K(EPI_MUL); break;
       default: FER_BF16K(EPI_GEN); break;
@@ -1506,6 +1542,7 @@ static int launch_8ph(GemmArgs g, const EpiArgs& e, hipStream_t st) {
     switch (ek) {                                      \
       case EPI_STORE: FER_8PH(DY, EPI_STORE); break;   \
       case EPI_GATE: FER_8PH(DY, EPI_GATE); break;     \
+      case EPI_GATER: FER_8PH(DY, EPI_GATER); break;   \
       case EPI_RES: FER_8PH(DY, EPI_RES); break;       \
       case EPI_MUL: FER_8PH(DY, EPI_MUL); break;       \
       case EPI_RES2: FER_8PH(DY, EPI_RES2); break;     \

@@ -1140,7 +1140,12 @@ extern "C" int fer_adamw(float* param, const float* grad, float* exp_avg, float*
                          const fer_adamw_segment* segs_device, int nsegs, int64_t max_seg_numel, float grad_scale,
                          const float* clip_coef, const uint64_t* step_add, fer_stream_t stream) {
   if (nsegs <= 0) return 0;
-  dim3 grid((unsigned)std::max<long>(1, std::min<long>((max_seg_numel + 1023) / 1024, 1024)), nsegs);
+  // blocks per segment: enough for the largest one to stream at full rate (the grid-stride loop
+  // covers the rest); every block of a smaller segment past its end exits at once, and with one
+  // block per 1024 elements of the largest segment those empty blocks (~80 % of a latent-ViT
+  // launch's 82 k blocks) cost more than the update itself
+  const long per_seg = std::max<long>(8, std::min<long>(256, 32768 / std::max(1, nsegs)));
+  dim3 grid((unsigned)std::max<long>(1, std::min<long>((max_seg_numel + 1023) / 1024, per_seg)), nsegs);
   hipLaunchKernelGGL(adamw_kernel, grid, dim3(256), 0, (hipStream_t)stream, param, grad, exp_avg, exp_avg_sq,
                      (bf16*)param_bf16, segs_device, grad_scale, clip_coef, step_add);
   return hip_check("adamw");

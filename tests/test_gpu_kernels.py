@@ -211,6 +211,13 @@ def test_gemm_8phase_epilogue_kinds(p, cfg):
         a.backward(torch.ones_like(a))
         assert rel_err(y.cpu(), torch.where(keep, a.detach() / (1 - p), torch.zeros(()))) < 1e-2
         assert rel_err(gate.cpu(), torch.where(keep, hh.grad / (1 - p), torch.zeros(()))) < 1e-2
+        # EPI_GATER: fc1 fwd of the ReLU encoders (LatentViT), pre = (h > 0) * keep / (1 - p)
+        gr = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        yr = o.linear_fwd(bf(x), bf(w), b.to(DEV), pre=gr, pre_gate=True, act="relu", dropout=p, seed=seed,
+                          drop_ld=N)
+        assert rel_err(yr.cpu(), torch.where(keep, torch.relu(h) / (1 - p), torch.zeros(()))) < 1e-2
+        gref = torch.where(keep & (h > 0), torch.full_like(h, 1 / (1 - p)), torch.zeros(())).to(torch.bfloat16)
+        assert (gr.cpu() != gref).float().mean().item() < 1e-3  # sign flips of |h| ~ 0 only
         # EPI_RES2: out-proj / fc2 fwd, bias + dropout + residual (and the residual-only dgrad form)
         z = o.linear_fwd(bf(x), bf(w), b.to(DEV), res=bf(r), dropout=p, seed=seed, drop_ld=N)
         assert rel_err(z.cpu(), torch.where(keep, h / (1 - p), torch.zeros(())) + rr) < 1e-2
