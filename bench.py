@@ -134,10 +134,12 @@ class GemmProbe:
 
     def __init__(self):
         self.rec = []
+        self.other = []  # FERVIT_PROBE_ALL=1: every other GEMM launch too (stderr table, not the JSON line)
+        self.all = os.environ.get("FERVIT_PROBE_ALL") == "1"
         self.on = False
 
     def __call__(self, d, e, launch):
-        if not self.on or not is_8ph(d):
+        if not self.on or not (is_8ph(d) or self.all):
             return launch()
         s = torch.cuda.current_stream()
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -149,8 +151,23 @@ class GemmProbe:
                                  ("gate" if gate else "pre", e.pre), ("x gate" if e.aux_act == 3 else "act'", e.aux),
                                  ("res", e.res), ("colsum", e.colsum)) if on]
         kind = "epi:" + ("+".join(parts) or "none")
+        if not is_8ph(d):
+            lay = ("K" if d.a_kc else "M") + ("K" if d.b_kc else "N")
+            self.other.append(((d.M, d.N, d.K), f"{lay} {kind}", 2.0 * d.M * d.N * d.K, a, b))
+            return r
         self.rec.append(((d.M, d.N, d.K), kind, 2.0 * d.M * d.N * d.K, gemm_algo_bytes(d, e), a, b))
         return r
+
+    def other_table(self, steps):
+        shapes = {}
+        for (mnk, kind, fl, a, b) in self.other:
+            c = shapes.setdefault(f"{mnk[0]}x{mnk[1]}x{mnk[2]} {kind}", [0, 0.0, fl])
+            c[0] += 1
+            c[1] += a.elapsed_time(b)
+        lines = [f"{v[1] / max(1, steps) * 1e3:9.1f} us/step {v[0] // max(1, steps):4d}x {1e3 * v[1] / v[0]:8.1f} us "
+                 f"{v[2] / (v[1] / v[0] / 1e3) / 1e12:7.1f} TF/s  {k}" for k, v in sorted(shapes.items(), key=lambda kv: -kv[1][1])]
+        tot = sum(v[1] for v in shapes.values()) / max(1, steps)
+        return "\n".join(lines + [f"other GEMM launches (each alone, incl. split-K reduce): {tot:.3f} ms/step"])
 
     def summary(self, steps):
         tot_ms = sum(a.elapsed_time(b) for *_, a, b in self.rec)
@@ -454,6 +471,8 @@ def main():
     probe.on = False
     runtime.WGRAD.enabled = wg_on
     ps = probe.summary(args.probe_steps)
+    if probe.all and rank == 0:
+        print(probe.other_table(args.probe_steps), file=sys.stderr, flush=True)
     ms = el / args.steps * 1e3
     imgs = world * B * args.steps / el
     step_tflops = flops_img * B / (ms / 1e3) / 1e12

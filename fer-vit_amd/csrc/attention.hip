@@ -1494,6 +1494,17 @@ static int n_cus() {
   return n;
 }
 
+// Workgroups per CU a persistent attention kernel can hold (registers / LDS; the occupancy API,
+// queried once per instantiation): the small-N instantiations (w+ latents: N = 19, one key block)
+// are one or two waves and fit several to a CU, so their persistent grid is CUs x this, not CUs --
+// one wave per CU left the latent-ViT attention latency-bound.
+template <typename Kern>
+static int pers_occ(Kern k, int threads) {
+  int n = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, threads, 0) != hipSuccess || n < 1) n = 1;
+  return std::min(n, 8);
+}
+
 extern "C" int64_t fer_attention_saved_floats(int dtype, int B, int N, int H, int dh, uint32_t drop_thresh) {
   const int64_t nb = (N + 31) / 32;
   const int64_t mask_words = (drop_thresh && pers_path(dtype, N, dh)) ? (int64_t)B * H * nb * nb * 32 : 0;
@@ -1532,7 +1543,15 @@ extern "C" int fer_attention_fwd(int dtype, const void* qkv, int64_t ld_qkv, voi
   } else if (N <= 224 && dh <= 64) {
     const int nb = (N + 31) / 32;
     uint32_t* mask = (drop_thresh && pers_path(dtype, N, dh)) ? (uint32_t*)(lse + lse_floats(B, N, H)) : nullptr;
-    const int grid = std::min(B * H, n_cus());
+    int occ = 1;
+#define FER_FOCC(NBV)                                                               \
+  case NBV: {                                                                       \
+    static const int o = pers_occ(attn_fwd_pers<NBV>, 64 * (NBV + 1));             \
+    occ = o;                                                                        \
+  } break;
+    switch (nb) { FER_FOCC(1) FER_FOCC(2) FER_FOCC(3) FER_FOCC(4) FER_FOCC(5) FER_FOCC(6) FER_FOCC(7) }
+#undef FER_FOCC
+    const int grid = std::min(B * H, n_cus() * occ);
     const WqArgs wq = fixed_stride() ? WqArgs{} : wq_prepare_here(st, grid, B * H);
 #define FER_FPERS(NBV)                                                                                       \
   case NBV:                                                                                                  \
@@ -1604,7 +1623,15 @@ extern "C" int fer_attention_bwd(int dtype, const void* qkv, int64_t ld_qkv, con
   static const bool old_bwd = getenv("FERVIT_ATTN_BWD_OLD") != nullptr;  // A/B switch (p = 0 only)
   if (pers_path(dtype, N, dh) && !general && !(old_bwd && !drop_thresh)) {
     const uint32_t* mask = drop_thresh ? (const uint32_t*)(lse + lse_floats(B, N, H)) : nullptr;
-    const int grid = std::min(B * H, n_cus());
+    int occ = 1;
+#define FER_BOCC(NBV)                                                               \
+  case NBV: {                                                                       \
+    static const int o = pers_occ(attn_bwd_pers<NBV>, 64 * NBV);                   \
+    occ = o;                                                                        \
+  } break;
+    switch (nb) { FER_BOCC(1) FER_BOCC(2) FER_BOCC(3) FER_BOCC(4) FER_BOCC(5) FER_BOCC(6) FER_BOCC(7) }
+#undef FER_BOCC
+    const int grid = std::min(B * H, n_cus() * occ);
     const WqArgs wq = fixed_stride() ? WqArgs{} : wq_prepare_here(st, grid, B * H);
 #define FER_PERS(NBV)                                                                                          \
   case NBV:                                                                                                    \

@@ -1660,14 +1660,22 @@ int gemm_launch(const GemmDesc& d, const EpiArgs& e_in, hipStream_t st) {
     if (max_splits < 2 || d.K < 1024 || tiles >= target) return 1;
     return (int)std::max<long>(1, std::min<long>({target / tiles, d.K / 256, (long)max_splits}));
   };
+  // split targets (workgroups per launch) of the 256^2 / 128^2 tile configs; FERVIT_GEMM_SPLIT_T256 /
+  // FERVIT_GEMM_SPLIT_T128 override them (tuning runs only)
+  static const long tgt256 = getenv("FERVIT_GEMM_SPLIT_T256") ? atol(getenv("FERVIT_GEMM_SPLIT_T256")) : 256;
+  // (128^2, K-contiguous: split only below half a round; the ordered slab reduction costs more than the
+  // idle CUs of an unsplit 152-228 tile grid -- latent fc2 fwd 50.7 -> 29.4 us, qkv dgrad 46.4 -> 22.9 us)
+  static const long tgt128 = getenv("FERVIT_GEMM_SPLIT_T128") ? atol(getenv("FERVIT_GEMM_SPLIT_T128")) : 512;
+  static const bool t128_env = getenv("FERVIT_GEMM_SPLIT_T128") != nullptr;
+  const long tgt128k = t128_env ? tgt128 : ((d.a_kc && d.b_kc) ? 256 : 512);
   int cfg = forced_cfg();
   if (cfg < 0) {
     if (d.K >= 8192 || t256 >= 256)  // big grids, and token-long weight gradients (split-K fills the GPU)
-      cfg = t256 * splits_for(t256, 256) >= 128 ? (!d.a_kc && !d.b_kc ? 5 : 8) : 3;
+      cfg = t256 * splits_for(t256, tgt256) >= 128 ? (!d.a_kc && !d.b_kc ? 5 : 8) : 3;
     else  // fewer 256^2 tiles than CUs (latent / 48 px configs): 128^2 tiles, two workgroups per CU
       cfg = 3;
   }
-  int splits = cfg_is_256(cfg) ? splits_for(t256, 256) : splits_for(t128, 512);
+  int splits = cfg_is_256(cfg) ? splits_for(t256, tgt256) : splits_for(t128, tgt128k);
   g.splits = splits;
   g.k_chunk = splits > 1 ? (((d.K + splits - 1) / splits + BK - 1) / BK) * BK : d.K;
   if (splits > 1) g.splits = (d.K + g.k_chunk - 1) / g.k_chunk;

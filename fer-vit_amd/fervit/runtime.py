@@ -235,19 +235,28 @@ class _WgradStream:
     to the compute stream while the side stream reads it, and the first use in a backward
     queues an autograd-engine callback that makes the compute stream wait for the side stream
     before backward returns (optimizer, clipping and user code then see finished gradients).
-    Off under HIP-graph capture and with FERVIT_WGRAD_STREAM=0 (same stream as the dgrads)."""
+    Under HIP-graph capture (StepGraph) the side stream forks from the capturing stream through
+    the same event wait and is joined back by the same callback, so the captured graph keeps the
+    two branches -- with FERVIT_WGRAD_CAPTURE=1 only: measured on the graph-replayed configs
+    (r03m, one box) it did not pay (w+ latent ViT 3.07 -> 3.04 ms, hybrid 7.09 -> 7.22 ms, 48 px
+    ImageViT 1.65 -> 1.75 ms), so captured steps keep one branch by default. Off entirely with
+    FERVIT_WGRAD_STREAM=0 (same stream as the dgrads)."""
 
     def __init__(self):
         self.streams = {}
         self.join_queued = False
         self.enabled = os.environ.get("FERVIT_WGRAD_STREAM", "1") != "0"
+        self.in_capture = os.environ.get("FERVIT_WGRAD_CAPTURE", "0") == "1"
+
+    def _off(self) -> bool:
+        return not self.enabled or (not self.in_capture and torch.cuda.is_current_stream_capturing())
 
     def stream(self, device):
         return self.streams.get(device)
 
     def run(self, fn, *inputs):
         dev = inputs[0].device
-        if not self.enabled or torch.cuda.is_current_stream_capturing():
+        if self._off():
             return fn()
         main = torch.cuda.current_stream(dev)
         side = self.streams.get(dev)
@@ -272,7 +281,7 @@ class _WgradStream:
 
     def sync(self):
         """The current (compute) stream waits for every weight gradient issued so far."""
-        if not self.streams or torch.cuda.is_current_stream_capturing():
+        if not self.streams or (not self.in_capture and torch.cuda.is_current_stream_capturing()):
             return
         for dev, side in self.streams.items():
             torch.cuda.current_stream(dev).wait_stream(side)

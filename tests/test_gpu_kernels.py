@@ -351,11 +351,12 @@ def test_attention_fwd_bwd(N, H, dh, dtype, p):
     assert torch.equal(dqkv2, dqkv) and torch.equal(cs2, cs)
 
 
-@pytest.mark.parametrize("N,H,dh,B", [(197, 12, 64, 64), (19, 8, 64, 128)])
+@pytest.mark.parametrize("N,H,dh,B", [(197, 12, 64, 64), (19, 8, 64, 512)])
 @pytest.mark.parametrize("p", [0.0, 0.1])
 def test_attention_persistent_multi_unit(N, H, dh, B, p):
     """The headline configuration's persistent attention path with several (batch, head) units per
-    workgroup: B*H = 768 / 1024 units on <= 256 workgroups, so every workgroup walks >= 3 units
+    workgroup: B*H = 768 units on 256 workgroups (N = 197) / 4096 units on CUs x occupancy <= 1024
+    workgroups (N = 19: several one-wave workgroups per CU), so every workgroup walks >= 3 units
     (next-unit K/V prefetch into the second LDS buffer, work-queue claims). Forward output, lse,
     the stored keep bits, dQ/dK/dV and the fused in_proj bias gradient against a torch fp32
     reference on the GPU, under the work queue (mode 0) and the fixed stride (mode 1), which must
