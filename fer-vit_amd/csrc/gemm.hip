@@ -1471,6 +1471,163 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs g, EpiArgs e, in
   }
 }
 
+// ============================================================ grouped weight gradients
+// dW_i (+)= dY_i^T X_i for the weight gradients of one encoder layer in ONE launch (fer_wgrad_group):
+// the small-token configurations (w+ latents: 4,864 rows, 48 px images: 640) have 16-64 output tiles
+// per weight, so each weight gradient alone needed split-K (fp32 slabs + a separate ordered
+// reduction launch) and still ran latency-bound (a 10 GF GEMM in ~40 us). Grouped, the layer's
+// 100-200 128x128 tiles fill the chip with little or no K split. Both operands are MN-contiguous
+// (token rows), read by LDS-DMA into an NST-slot ring of BK=64 stages, ds_read_b64_tr_b16
+// fragments, v_mfma_f32_16x16x32_bf16, 2 x WN waves. Output written straight from the accumulators
+// (fp32 rows of 4, accumulate optional).
+// K split (splits > 1): every split writes its partial tile to a tile-local fp32 slab with
+// write-through (sc1) stores, drains them, and takes a ticket from the tile's counter (agent-scope
+// atomic, zeroed by the host per launch); the split that draws the last ticket sums the tile's
+// slabs in split order -- its own partial from registers at its own position, the others by sc1
+// loads -- and writes dW (MI355X_MICROARCH.md, Workgroup dispatch: the sc1-store / counter /
+// sc1-load hand-off, one workgroup per CU). Deterministic for any arrival order.
+constexpr int WG_MAX = 8;
+struct WgItem {
+  const bf16* A;  // dY [K tokens][M], row stride lda
+  const bf16* B;  // X  [K tokens][N], row stride ldb
+  float* C;       // dW [M][N], row stride ldc
+  long lda, ldb, ldc;
+  int M, N, tiles_m, tile0, acc;
+};
+struct WgGroup {
+  WgItem it[WG_MAX];
+  int n, K, splits, k_chunk;
+  unsigned* cnt;  // [tiles] tickets (zeroed by the host before the launch)
+  float* slab;    // [tiles][splits][128*128]
+};
+
+template <int NST, int WN>
+__global__ __launch_bounds__(128 * WN, 1) void gemm_wgrad_group_kernel(WgGroup grp) {
+  constexpr int BM = 128, BN = 128, NW = 2 * WN, MT = 16, TM = 64, TN = 128 / WN, FM = TM / MT, FN = TN / MT;
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
+  __shared__ __attribute__((aligned(1024))) char smem[NST * STAGE + 16];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave & 1, wn = wave >> 1;  // 2 x WN waves of 64 x TN
+  const int tl = blockIdx.x, ks = blockIdx.y;
+  int ii = 0;
+#pragma unroll
+  for (int i = 1; i < WG_MAX; ++i)
+    if (i < grp.n && tl >= grp.it[i].tile0) ii = i;
+  const WgItem& it = grp.it[ii];
+  const int t = tl - it.tile0;
+  const int tm = t % it.tiles_m, tn = t / it.tiles_m;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int kbeg = ks * grp.k_chunk;
+  const int kend = min(grp.K, kbeg + grp.k_chunk);
+  const int nk = (kend - kbeg + BK - 1) / BK;
+  const int ktail = kbeg + (nk - 1) * BK;
+
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(it.A);
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(it.B);
+  typedef DmaPlan<BM, false, NW, MT> PA;
+  typedef DmaPlan<BN, false, NW, MT> PB;
+  PA pa;
+  PB pb;
+  pa.init(wave, lane, it.lda, m0, it.M);
+  pb.init(wave, lane, it.ldb, n0, it.N);
+  constexpr int PER = PA::NI + PB::NI;  // DMA instructions per stage per wave
+  auto slot = [&](int st) -> char* { return smem + (st % NST) * STAGE; };
+  auto issue = [&](int st) {
+    const int k0 = kbeg + st * BK;
+    pa.issue(ra, slot(st), wave, it.lda, k0, kend, k0 == ktail);
+    pb.issue(rb, slot(st) + A_BYTES, wave, it.ldb, k0, kend, k0 == ktail);
+  };
+
+  f32x4 acc[FN][FM];
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int j = 0; j < FM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int st = 0; st < NST - 1; ++st)
+    if (st < nk) issue(st);
+  for (int k = 0; k < nk; ++k) {
+    // stage k landed (this wave's pieces); up to NST-2 later stages stay in flight
+    const int ahead = min(NST - 2, nk - 1 - k);
+    if constexpr (NST >= 4) {
+      if (ahead >= 2) wait_vm<2 * PER>();
+      else if (ahead == 1) wait_vm<PER>();
+      else wait_vm<0>();
+    } else if constexpr (NST == 3) {
+      if (ahead >= 1) wait_vm<PER>();
+      else wait_vm<0>();
+    } else {
+      wait_vm<0>();
+    }
+    // every wave's pieces of stage k are in LDS, and every wave is done with stage k-1's slot
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (k + NST - 1 < nk) issue(k + NST - 1);
+    const char* cur = slot(k);
+    bf16x8 af[2][FM], bfr[2][FN];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+      for (int i = 0; i < FN; ++i) bfr[kk][i] = read_frag<MT, BN, false>(cur + A_BYTES, wn * TN + i * MT, kk, lane);
+#pragma unroll
+      for (int j = 0; j < FM; ++j) af[kk][j] = read_frag<MT, BM, false>(cur, wm * TM + j * MT, kk, lane);
+    }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int j = 0; j < FM; ++j)
+#pragma unroll
+        for (int i = 0; i < FN; ++i) acc[i][j] = mfma<MT>(bfr[kk][i], af[kk][j], acc[i][j]);
+  }
+
+  // accumulator (i, j): rows m0 + wm*64 + 16j + (lane & 15), columns n0 + wn*64 + 16i + 4(lane >> 4) + 0..3
+  const int lr = lane & 15, lc = 4 * (lane >> 4);
+  if (grp.splits > 1) {
+    const int S = grp.splits;
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(grp.slab + (long)tl * S * (BM * BN));
+    auto soff = [&](int sp, int i, int j) -> uint32_t {
+      return (uint32_t)(((sp * BM + wm * TM + j * MT + lr) * BN + wn * TN + i * MT + lc) * 4);
+    };
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+      for (int j = 0; j < FM; ++j) __builtin_amdgcn_raw_buffer_store_b128(
+          __builtin_bit_cast(u32x4, acc[i][j]), rs, soff(ks, i, j), 0, 16 /* sc1: write-through */);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drained
+    __syncthreads();
+    volatile unsigned* flag = (volatile unsigned*)(smem + NST * STAGE);
+    if (threadIdx.x == 0)
+      *flag = __hip_atomic_fetch_add(grp.cnt + tl, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (*flag != (unsigned)(S - 1)) return;  // not the last split of this tile
+    // last split: slabs in split order (sc1 loads: every load of the handed-off bytes)
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+      for (int j = 0; j < FM; ++j) {
+        f32x4 sum = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int sp = 0; sp < S; ++sp) {
+          const f32x4 v = sp == ks ? acc[i][j]
+                                   : __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, soff(sp, i, j), 0, 16));
+          sum = sp == 0 ? v : sum + v;
+        }
+        acc[i][j] = sum;
+      }
+  }
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int j = 0; j < FM; ++j) {
+      const long m = m0 + wm * TM + j * MT + lr, n = n0 + wn * TN + i * MT + lc;
+      if (m < it.M && n < it.N) {
+        f32x4* c = (f32x4*)(it.C + m * it.ldc + n);
+        *c = it.acc ? *c + acc[i][j] : acc[i][j];
+      }
+    }
+}
+
 // -------------------------------------------------------------------- launch
 template <int BM, int BN, int WM, int WN, bool AKC, bool BKC, int MT>
 static int launch_bf16(GemmArgs g, const EpiArgs& e, hipStream_t st) {
@@ -1701,6 +1858,92 @@ int gemm_launch(const GemmDesc& d, const EpiArgs& e_in, hipStream_t st) {
                      (long)d.N, e);
   return hip_check("splitk_reduce");
 }
+
+// ---- grouped weight gradients (fer_wgrad_group)
+namespace {
+int wg_splits(int tiles, int K, int req) {
+  if (req > 0) return std::min(req, 8);
+  static const int env = getenv("FERVIT_WG_SPLITS") ? atoi(getenv("FERVIT_WG_SPLITS")) : 0;  // tuning runs
+  if (env > 0) return std::min(env, 8);
+  int dev = 0, ncu = 256;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    ncu = 256;
+  // two 64 KB-ring workgroups per CU: split K while the grid stays within one round of those
+  return std::max(1, std::min({2 * ncu / std::max(1, tiles), K / 1024, 8}));
+}
+long wg_tiles(const fer_wgrad_item* it, int n) {
+  long t = 0;
+  for (int i = 0; i < n; ++i) t += (long)((it[i].N + 127) / 128) * ((it[i].K + 127) / 128);
+  return t;
+}
+}  // namespace
+}  // namespace fer
+
+extern "C" int64_t fer_wgrad_group_ws(const fer_wgrad_item* items, int n, int splits) {
+  if (!items || n <= 0) return 0;
+  const long tiles = fer::wg_tiles(items, n);
+  const int S = fer::wg_splits((int)tiles, items[0].M, splits);
+  return S > 1 ? tiles * S * 128 * 128 * 4 + tiles * 4 + 64 : 0;
+}
+
+extern "C" int fer_wgrad_group(const fer_wgrad_item* items, int n, int splits, float* ws, int64_t ws_bytes,
+                               fer_stream_t stream) {
+  using namespace fer;
+  if (n <= 0) return 0;
+  if (!items || n > WG_MAX) return set_error("wgrad_group: 1..8 items");
+  hipStream_t st = (hipStream_t)stream;
+  WgGroup g{};
+  g.n = n;
+  g.K = items[0].M;
+  int tile0 = 0;
+  for (int i = 0; i < n; ++i) {
+    const fer_wgrad_item& x = items[i];
+    if (x.M != g.K) return set_error("wgrad_group: every item needs the same token count M");
+    if (x.M <= 0 || x.N <= 0 || x.K <= 0) return set_error("wgrad_group: empty item");
+    if (x.N % 8 || x.K % 8 || x.ld_dy % 8 || x.ld_x % 8 || x.ld_dw % 4 || x.ld_dy < x.N || x.ld_x < x.K ||
+        x.ld_dw < x.K || (uintptr_t)x.dy % 16 || (uintptr_t)x.x % 16 || (uintptr_t)x.dw % 16)
+      return set_error("wgrad_group: N, K and the row strides need 8-element (16-byte) alignment");
+    if ((long)(x.M - 1) * x.ld_dy * 2 + 2L * x.N >= 0x7FFFFFF0L || (long)(x.M - 1) * x.ld_x * 2 + 2L * x.K >= 0x7FFFFFF0L)
+      return set_error("wgrad_group: operand exceeds 2 GiB");
+    WgItem& w = g.it[i];
+    w.A = (const bf16*)x.dy; w.lda = x.ld_dy;
+    w.B = (const bf16*)x.x; w.ldb = x.ld_x;
+    w.C = x.dw; w.ldc = x.ld_dw;
+    w.M = x.N; w.N = x.K;
+    w.tiles_m = (x.N + 127) / 128;
+    w.tile0 = tile0;
+    w.acc = x.accumulate;
+    tile0 += w.tiles_m * ((x.K + 127) / 128);
+  }
+  int S = wg_splits(tile0, g.K, splits);
+  g.splits = S;
+  g.k_chunk = S > 1 ? ((g.K + S - 1) / S + BK - 1) / BK * BK : g.K;
+  if (S > 1) {
+    g.splits = S = (g.K + g.k_chunk - 1) / g.k_chunk;
+    const long need = (long)tile0 * S * 128 * 128 * 4 + (long)tile0 * 4;
+    if (!ws || ws_bytes < need) return set_error("wgrad_group: workspace smaller than fer_wgrad_group_ws()");
+    g.slab = ws;
+    g.cnt = (unsigned*)((char*)ws + (long)tile0 * S * 128 * 128 * 4);
+    if (hipMemsetAsync(g.cnt, 0, (size_t)tile0 * 4, st) != hipSuccess) return set_error("wgrad_group: memset failed");
+  }
+  // Shipped: 4 waves of 64x64, 2-slot ring (64 KB: two workgroups per CU, whose stage latencies
+  // interleave), K split to ~2 workgroups per CU. Latent-ViT layer (4 weights, 192 tiles, K 4864):
+  // 57 us vs 74-77 us for the 4-slot ring (one workgroup per CU) with 4 or 8 waves at any split,
+  // and 189 us as four split-K launches (profiles/r03o_wgrad_group_variants.txt).
+  // FERVIT_WG_VARIANT (tuning runs): 1 = 8 waves 4-slot, 2 = 8 waves 2-slot, 4 = 4 waves 4-slot.
+  static const int var = getenv("FERVIT_WG_VARIANT") ? atoi(getenv("FERVIT_WG_VARIANT")) : 0;
+  if (var == 1)
+    hipLaunchKernelGGL((gemm_wgrad_group_kernel<4, 4>), dim3(tile0, S), dim3(512), 0, st, g);
+  else if (var == 2)
+    hipLaunchKernelGGL((gemm_wgrad_group_kernel<2, 4>), dim3(tile0, S), dim3(512), 0, st, g);
+  else if (var == 4)
+    hipLaunchKernelGGL((gemm_wgrad_group_kernel<4, 2>), dim3(tile0, S), dim3(256), 0, st, g);
+  else
+    hipLaunchKernelGGL((gemm_wgrad_group_kernel<2, 2>), dim3(tile0, S), dim3(256), 0, st, g);
+  return hip_check("wgrad_group");
+}
+
+namespace fer {
 
 }  // namespace fer
 

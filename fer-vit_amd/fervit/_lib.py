@@ -33,6 +33,11 @@ class Epilogue(C.Structure):
                 ("colsum_accumulate", i32)]
 
 
+class WgradItem(C.Structure):
+    _fields_ = [("dy", vp), ("ld_dy", i64), ("x", vp), ("ld_x", i64), ("dw", vp), ("ld_dw", i64),
+                ("M", i32), ("N", i32), ("K", i32), ("accumulate", i32)]
+
+
 class AdamWSegment(C.Structure):
     _fields_ = [("offset", i64), ("numel", i64), ("lr", f32), ("weight_decay", f32), ("beta1", f32),
                 ("beta2", f32), ("eps", f32), ("step", i32)]
@@ -49,6 +54,8 @@ SIGNATURES = {
     "fer_gemm_set_config": (i32, [i32]),
     "fer_set_persistent_mode": (i32, [i32]),
     "fer_gemm_colsum_ws": (i64, [i32, i32]),
+    "fer_wgrad_group": (i32, [C.POINTER(WgradItem), i32, i32, fp, i64, vp]),
+    "fer_wgrad_group_ws": (i64, [C.POINTER(WgradItem), i32, i32]),
     "fer_layernorm_fwd": (i32, [i32, vp, i64, fp, fp, i32, i32, vp, i64, fp, fp, i32, i32, f32, vp]),
     "fer_layernorm_bwd_ws": (i64, [i32, i32]),
     "fer_layernorm_bwd": (i32, [i32, vp, i64, vp, i64, fp, fp, fp, i32, i32, vp, i64, vp, i64, vp, u32, f32, u64,

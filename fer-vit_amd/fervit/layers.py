@@ -19,6 +19,8 @@ from __future__ import annotations
 from dataclasses import dataclass
 from typing import List, Optional, Sequence
 
+import os
+
 import torch
 
 from . import ops
@@ -81,6 +83,32 @@ def _wgrad(dy, x, out, **kw):
     return WGRAD.run(lambda: ops.linear_wgrad(dy, x, out, **kw), dy, x)
 
 
+# Token counts up to which a layer's weight gradients go out as ONE grouped launch at the end of
+# its backward (csrc/gemm.hip gemm_wgrad_group_kernel) instead of one split-K GEMM (+ reduction)
+# each: the w+ latent (4,864 rows) and 48 px (640) configurations. ViT-B/16 (50,432 rows) keeps
+# the per-weight split-K launches, issued as soon as each dY exists.
+WGRAD_GROUP_MAX_M = int(os.environ.get("FERVIT_WGRAD_GROUP_MAX_M", "16384"))
+
+
+class _WgradBatch:
+    def __init__(self, M: int, dt: torch.dtype):
+        self.on = dt == torch.bfloat16 and M <= WGRAD_GROUP_MAX_M
+        self.items = []
+
+    def add(self, dy, x, out, accumulate: bool) -> None:
+        if out is None:
+            return
+        if self.on:
+            self.items.append((dy, x, out, accumulate))
+        else:
+            _wgrad(dy, x, out, accumulate=accumulate)
+
+    def flush(self) -> None:
+        if self.items:
+            items, self.items = self.items, []
+            WGRAD.run(lambda: ops.linear_wgrad_group(items), *[t for it in items for t in it[:2]])
+
+
 def _empty(M, N, like, dtype=None):
     return torch.empty(M, N, dtype=dtype or like.dtype, device=like.device)
 
@@ -133,18 +161,17 @@ class PostNormLayerFn(torch.autograd.Function):
         dt = x.dtype
         dh = D // cfg.H
         pd = cfg.dropout
+        wb = _WgradBatch(M, dt)
         # LN2 (+ dropout of the FFN branch, + linear2 bias grad)
         dz = torch.empty_like(z)
         dh2 = torch.empty_like(z) if pd > 0 else None
         ops.layernorm_bwd(dout, z, m2, r2, n2w.data, dx=dz, dx_drop=dh2, dropout=pd, seed=seeds[3], dgamma=gn2w,
                           dbeta=gn2b, dbias=gb2, accumulate=acc)
         dh2 = dz if dh2 is None else dh2
-        if gw2 is not None:
-            _wgrad(dh2, g, gw2, accumulate=acc)
+        wb.add(dh2, g, gw2, acc)
         # linear1.bias grad = column sums of dF, fused into this GEMM's epilogue
         dF = _dgrad(flat, dh2, w2, dt, aux=f, aux_act="mul", colsum=gb1, colsum_accumulate=acc)
-        if gw1 is not None:
-            _wgrad(dF, x1, gw1, accumulate=acc)
+        wb.add(dF, x1, gw1, acc)
         dx1 = _dgrad(flat, dF, w1, dt, res=dz)
         # LN1 (+ dropout of the attention branch, + out_proj bias grad)
         dy = torch.empty_like(y)
@@ -152,15 +179,14 @@ class PostNormLayerFn(torch.autograd.Function):
         ops.layernorm_bwd(dx1, y, m1, r1, n1w.data, dx=dy, dx_drop=dhh, dropout=pd, seed=seeds[1], dgamma=gn1w,
                           dbeta=gn1b, dbias=gout_b, accumulate=acc)
         dhh = dy if dhh is None else dhh
-        if gout_w is not None:
-            _wgrad(dhh, o, gout_w, accumulate=acc)
+        wb.add(dhh, o, gout_w, acc)
         do = _dgrad(flat, dhh, out_w, dt)
         dqkv = _empty(M, 3 * D, x)
         ops.attention_bwd(qkv, o, do, lse, dqkv, cfg.B, cfg.N, cfg.H, dh, dropout=pd, seed=seeds[0], colsum=gin_b,
                           colsum_accumulate=acc)
-        if gin_w is not None:
-            _wgrad(dqkv, x, gin_w, accumulate=acc)
+        wb.add(dqkv, x, gin_w, acc)
         dx = _dgrad(flat, dqkv, in_w, dt, res=dy)
+        wb.flush()
         _finish(flat, P, needs)
         ctx.saved = None
         return (dx, None, None) + (None,) * len(P)
@@ -208,26 +234,24 @@ class PreNormBlockFn(torch.autograd.Function):
         M, D = x.shape
         dt = x.dtype
         dh = D // cfg.H
+        wb = _WgradBatch(M, dt)
         if gfc2_b is not None:
             ops.colsum(dout, gfc2_b, accumulate=acc)
-        if gfc2_w is not None:
-            _wgrad(dout, g, gfc2_w, accumulate=acc)
+        wb.add(dout, g, gfc2_w, acc)
         dF = _dgrad(flat, dout, fc2_w, dt, aux=f, aux_act="mul", colsum=gfc1_b, colsum_accumulate=acc)
-        if gfc1_w is not None:
-            _wgrad(dF, h2, gfc1_w, accumulate=acc)
+        wb.add(dF, h2, gfc1_w, acc)
         dh2 = _dgrad(flat, dF, fc1_w, dt)
         dx2 = ops.layernorm_bwd(dh2, x2, m2, r2, n2w.data, res=dout, dgamma=gn2w, dbeta=gn2b, accumulate=acc)
         if gproj_b is not None:
             ops.colsum(dx2, gproj_b, accumulate=acc)
-        if gproj_w is not None:
-            _wgrad(dx2, o, gproj_w, accumulate=acc)
+        wb.add(dx2, o, gproj_w, acc)
         do = _dgrad(flat, dx2, proj_w, dt)
         dqkv = _empty(M, 3 * D, x)
         ops.attention_bwd(qkv, o, do, lse, dqkv, cfg.B, cfg.N, cfg.H, dh, colsum=gqkv_b, colsum_accumulate=acc)
-        if gqkv_w is not None:
-            _wgrad(dqkv, h1, gqkv_w, accumulate=acc)
+        wb.add(dqkv, h1, gqkv_w, acc)
         dh1 = _dgrad(flat, dqkv, qkv_w, dt)
         dx = ops.layernorm_bwd(dh1, x, m1, r1, n1w.data, res=dx2, dgamma=gn1w, dbeta=gn1b, accumulate=acc)
+        wb.flush()
         _finish(flat, P, needs)
         ctx.saved = None
         return (dx, None, None) + (None,) * len(P)

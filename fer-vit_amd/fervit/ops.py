@@ -156,6 +156,27 @@ def linear_dgrad(dy, w, out=None, **kw):
     return gemm(dy, w, out, a_kc=True, b_kc=False, M=M, N=K, K=N, lda=N, ldb=K, **kw)
 
 
+def linear_wgrad_group(items, splits: int = 0):
+    """dW_i (+)= dy_i^T x_i for several nn.Linear weights sharing the token count, in one launch
+    (csrc/gemm.hip gemm_wgrad_group_kernel). items: (dy [M,N] bf16, x [M,K] bf16, out fp32 [N,K],
+    accumulate) tuples; at most 8."""
+    n = len(items)
+    arr = (_lib.WgradItem * n)()
+    for i, (dy, x, out, acc) in enumerate(items):
+        _dev(dy)
+        if dy.dtype != torch.bfloat16 or x.dtype != torch.bfloat16 or out.dtype != torch.float32:
+            raise TypeError("linear_wgrad_group: bf16 dy / x and fp32 out")
+        M, N = dy.shape
+        K = x.shape[1]
+        if x.shape[0] != M or tuple(out.shape) != (N, K) or dy.stride(1) != 1 or x.stride(1) != 1 or out.stride(1) != 1:
+            raise ValueError("linear_wgrad_group: shapes / row-major layouts")
+        arr[i] = _lib.WgradItem(dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), out.data_ptr(), out.stride(0),
+                                M, N, K, int(bool(acc)))
+    nb = lib().fer_wgrad_group_ws(arr, n, splits)
+    w = WS.get(nb, items[0][0].device, slot=1) if nb > 0 else None
+    check(lib().fer_wgrad_group(arr, n, splits, ptr(w), 0 if w is None else w.numel() * 4, stream()), "wgrad_group")
+
+
 def linear_wgrad(dy, x, out, accumulate=False, **kw):
     """dW (+)= dy^T x for dy [M,N], x [M,K]; out fp32 [N,K]."""
     M, N = dy.shape

@@ -77,6 +77,22 @@ typedef struct {
 
 int fer_gemm(const fer_gemm_desc* d, const fer_epilogue* e, fer_stream_t stream);
 
+/* Grouped weight gradients: dw[n][k] (+)= sum_m dy[m][n] x[m][k] (bf16 dy [M][N] row stride ld_dy,
+ * bf16 x [M][K] row stride ld_x, fp32 dw [N][K] row stride ld_dw) for up to 8 nn.Linear weights
+ * that share the token count M, in one launch -- the weight-gradient half of nn.Linear's backward
+ * (`latent_vit.py:20,24-31`, `image_vit.py:101-113` TransformerEncoderLayer linears) for the
+ * small-token configurations, where each weight alone is too few output tiles to fill the GPU.
+ * splits: K (token) split per tile, 0 = automatic; a split run needs ws >= fer_wgrad_group_ws
+ * bytes (fp32 slabs + tile tickets; the reduction is in-launch, fixed split order). */
+typedef struct {
+  const void* dy; int64_t ld_dy;
+  const void* x; int64_t ld_x;
+  float* dw; int64_t ld_dw;
+  int M, N, K; int accumulate;
+} fer_wgrad_item;
+int fer_wgrad_group(const fer_wgrad_item* items, int n, int splits, float* ws, int64_t ws_bytes, fer_stream_t stream);
+int64_t fer_wgrad_group_ws(const fer_wgrad_item* items, int n, int splits);
+
 /* Workspace bytes fer_gemm needs for the fused column sums of an M x N output. */
 int64_t fer_gemm_colsum_ws(int M, int N);
 

@@ -296,6 +296,37 @@ def attn_ref(qkv, B, N, H, dh, keep=None, p=0.0):
     return out, lse
 
 
+@pytest.mark.parametrize("splits", [0, 1, 2, 3])
+def test_wgrad_group(splits):
+    """One grouped launch of several weight gradients sharing the token count (csrc/gemm.hip
+    gemm_wgrad_group_kernel): ragged tiles (N, K not multiples of 128), padded row strides,
+    accumulate on / off, K split 1-3 with the in-launch ordered reduction; against fp32 torch,
+    bit-identical on a repeat (the split reduction's order does not depend on arrival)."""
+    o = ops()
+    M = 1000
+    g = torch.Generator(device=DEV).manual_seed(11 + splits)
+    shapes = [(256, 128, False), (136, 200, True), (384, 512, False), (64, 8, True), (520, 264, False)]
+    items, refs = [], []
+    for N, K, acc in shapes:
+        dy = torch.randn(M, N + 8, device=DEV, generator=g).to(torch.bfloat16)[:, :N]  # row stride N + 8
+        x = torch.randn(M, K, device=DEV, generator=g).to(torch.bfloat16)
+        out = torch.randn(N, K, device=DEV, generator=g) if acc else torch.full((N, K), float("nan"), device=DEV)
+        ref = dy.float().t() @ x.float() + (out if acc else 0)
+        items.append((dy, x, out, acc))
+        refs.append(ref)
+    init = [it[2].clone() for it in items]
+    o.linear_wgrad_group(items, splits=splits)
+    torch.cuda.synchronize()
+    for (dy, x, out, acc), ref in zip(items, refs):
+        assert rel_err(out, ref) < 1e-5, (dy.shape, x.shape, acc)
+    first = [it[2].clone() for it in items]
+    for it, i0 in zip(items, init):
+        it[2].copy_(i0)
+    o.linear_wgrad_group(items, splits=splits)
+    for it, f in zip(items, first):
+        assert torch.equal(it[2], f)
+
+
 @pytest.mark.parametrize("N,H,dh", [(10, 8, 48), (19, 8, 64), (37, 12, 64), (197, 12, 64), (19, 6, 64), (100, 4, 64),
                                     (150, 3, 32), (250, 2, 64),
                                     # general path (csrc/attention.hip attn_*_gen): dh > 64 or N > 256

@@ -46,6 +46,10 @@ def main():
         "fc1_wgrad": (lambda: ops.linear_wgrad(h, x, gw["1"]), 2 * M * F * D),
         "fc2_wgrad": (lambda: ops.linear_wgrad(x, h, gw["2"]), 2 * M * F * D),
         "fc1_wgrad_kk": (lambda: ops.gemm(hT, xT, gw["1"], M=F, N=D, K=M), 2 * M * F * D),
+        # the layer's four weight gradients as one grouped launch (what the latent layers run)
+        "wgrad_group": (lambda: ops.linear_wgrad_group([(dq, x, gw["qkv"], False), (x, x, gw["o"], False),
+                                                        (h, x, gw["1"], False), (x, h, gw["2"], False)]),
+                        2 * M * (3 * D * D + D * D + 2 * F * D)),
     }
     only = os.environ.get("GB_ONLY")
     tag = os.environ.get("GB_TAG", "")
@@ -54,7 +58,7 @@ def main():
         if only and k not in only.split(","):
             continue
         t = min(timeit(fn) for _ in range(3))
-        if not k.endswith(("nodrop", "gelu", "_kk")):
+        if not k.endswith(("nodrop", "gelu", "_kk", "_group")):
             tot += t
         print(f"[{tag}] {k:15s} {t * 1e3:7.1f} us {fl / t / 1e12 * 1e3:7.1f} TF", flush=True)
     print(f"[{tag}] layer sum {tot * 1e3:.1f} us", flush=True)
