@@ -21,6 +21,7 @@ struct GemmArgs {
   float* ws;
   float* cs_part;  // fused column sums: per-tile partials [tiles_m][N] (or null)
   int dbg;  // experiment switches (FERVIT_GEMM_DBG), 0 in production
+  unsigned* cnt;  // split-K with the in-launch reduction: per-tile tickets (zeroed per launch), else null
   int* tq;               // persistent 8-phase kernel: work-queue counters (common.h wq_*), null = fixed stride
   unsigned tq_base[8];   // their values at launch
 };

@@ -535,7 +535,58 @@ FER_DEV void tile_epilogue(const GemmArgs& g, const EpiArgs& e, AccT (&acc)[FN][
   constexpr int NQ = MT == 32 ? 4 : 1;
   const int lr = MT == 32 ? (lane & 31) : (lane & 15);
   const int lc = MT == 32 ? 4 * (lane >> 5) : 4 * (lane >> 4);
-  if (g.partial) {  // split-K partial slab, fp32 [split][M][N]
+  if constexpr (EK == EPI_GEN) {
+    if (g.partial && g.cnt) {
+      // split-K, reduced in this launch: the partial goes to slab ks ([split][M][N] fp32) by
+      // write-through (sc1) stores; after every wave drained them, thread 0 takes a ticket from the
+      // tile's counter (agent-scope atomic; counters zeroed by the host before the launch). The split
+      // drawing the last ticket sums the tile's slabs by sc1 loads in split order and applies the
+      // epilogue -- the arithmetic of splitk_reduce_kernel element for element (bit-identical), with
+      // no second launch and the slabs still warm. (MI355X_MICROARCH.md, Workgroup dispatch: sc1
+      // stores / counter / sc1 loads, one workgroup per CU.)
+      const __amdgpu_buffer_rsrc_t rs = make_rsrc(g.ws);
+      const long MN = (long)g.M * g.N;
+#pragma unroll
+      for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int j = 0; j < FM; ++j)
+#pragma unroll
+          for (int q = 0; q < NQ; ++q) {
+            const long m = m0 + wm * TM + j * MT + lr, n = n0 + wn * TN + i * MT + 8 * q + lc;
+            if (m < g.M && n < g.N)
+              __builtin_amdgcn_raw_buffer_store_b128(
+                  __builtin_bit_cast(u32x4, f32x4{acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2],
+                                                  acc[i][j][4 * q + 3]}),
+                  rs, (uint32_t)((ks * MN + m * g.N + n) * 4), 0, 16 /* sc1 */);
+          }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's partial is out
+      __syncthreads();  // every wave's partial is out; every wave is past the main loop's LDS reads
+      volatile unsigned* flag = (volatile unsigned*)smem;
+      if (tid_ == 0)
+        *flag = __hip_atomic_fetch_add(g.cnt + (m0 / BM) + (n0 / BN) * g.tiles_m, 1u, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();
+      const bool last = *flag == (unsigned)(g.splits - 1);
+      __syncthreads();  // the flag word is read before any later use of the LDS (persistent kernels)
+      if (!last) return;
+      const uint64_t seed = e.drop_thresh ? step_seed(e.seed) : 0;
+      constexpr int G4 = BN / 4, NT = 64 * WM * WN;
+      const int rows = min(BM, g.M - m0), cols4 = min(BN, g.N - n0) / 4;
+#pragma unroll 1
+      for (int idx = tid_; idx < BM * G4; idx += NT) {
+        const int r = idx / G4, c = idx - r * G4;
+        if (r >= rows || c >= cols4) continue;
+        const long m = m0 + r, n = n0 + 4 * c;
+        const uint32_t o = (uint32_t)((m * g.N + n) * 4);
+        f32x4 v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 16));
+        for (int sp = 1; sp < g.splits; ++sp)
+          v += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, o + (uint32_t)(sp * MN * 4), 0, 16));
+        epi4<bf16>(e, m, n, v, seed);
+      }
+      return;
+    }
+  }
+  if (g.partial) {  // split-K partial slab, fp32 [split][M][N] (reduced by splitk_reduce_kernel)
     float* ws = g.ws + (long)ks * g.M * g.N;
 #pragma unroll
     for (int i = 0; i < FN; ++i)
@@ -1839,6 +1890,22 @@ int gemm_launch(const GemmDesc& d, const EpiArgs& e_in, hipStream_t st) {
   g.partial = g.splits > 1;
   g.ws = d.ws;
   g.cs_part = e.colsum ? d.ws : nullptr;
+  g.cnt = nullptr;
+  // in-launch split-K reduction (tile_epilogue; tickets after the slabs in the workspace, zeroed
+  // here) only with FERVIT_SPLITK_INLAUNCH=1: measured slower than the separate full-chip
+  // splitk_reduce launch -- the last split of a tile reads every slab of it alone on one CU
+  // (ViT-B fc1 wgrad 263 -> 310 us, step 36.3 -> 38.6 ms; latent 3-way split fc2 fwd 40 -> 55 us;
+  // profiles/r03q_splitk_inlaunch_ab.txt). The grouped weight gradients keep their in-launch
+  // reduction: two 64 KB slabs per tile there.
+  static const bool inlaunch = getenv("FERVIT_SPLITK_INLAUNCH") != nullptr;
+  if (g.partial && inlaunch) {
+    const long tiles = t128;  // >= the tile count of every configuration (tiles are >= 128 x 128)
+    const long slab_bytes = (long)g.splits * d.M * d.N * 4;
+    if (slab_bytes + tiles * 4 <= d.ws_bytes && slab_bytes < 0x7FFFFFF0L) {
+      g.cnt = (unsigned*)((char*)d.ws + slab_bytes);
+      if (hipMemsetAsync(g.cnt, 0, (size_t)tiles * 4, st) != hipSuccess) return set_error("gemm: ticket memset failed");
+    }
+  }
 
   if (d.a_kc && d.b_kc) dispatch_tile<true, true>(cfg, g, e, st);
   else if (d.a_kc && !d.b_kc) dispatch_tile<true, false>(cfg, g, e, st);
@@ -1851,7 +1918,7 @@ int gemm_launch(const GemmDesc& d, const EpiArgs& e_in, hipStream_t st) {
                 st);
     rc = hip_check("gemm_colsum_reduce");
   }
-  if (rc || !g.partial) return rc;
+  if (rc || !g.partial || g.cnt) return rc;
   const long work = (long)d.M * (d.N / 4);
   const int blocks = (int)std::min<long>((work + 255) / 256, 4096);
   hipLaunchKernelGGL(splitk_reduce_kernel<bf16>, dim3(blocks), dim3(256), 0, st, d.ws, g.splits, (long)d.M,

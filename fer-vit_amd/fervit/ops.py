@@ -101,7 +101,7 @@ def gemm(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, *, a_kc: bool = Tr
         d.ws, d.ws_bytes = w.data_ptr(), w.numel() * 4
     elif split_ws and d.dtype == 0 and K >= 1024 and t256 < 256:
         # split-K slabs: the library targets ~one 256x256 workgroup per CU (or 512 128^2 ones)
-        nb = 4 * M * N * min(32, max(2, 512 // t256))
+        nb = 4 * M * N * min(32, max(2, 512 // t256)) + 4 * (-(-M // 128) * -(-N // 128)) + 256  # + tile tickets
         w = WS.get(nb, A.device, slot=1)
         d.ws, d.ws_bytes = w.data_ptr(), w.numel() * 4
     e = Epilogue()
