@@ -1356,6 +1356,14 @@ FER_DEV void tile_8ph(const GemmArgs& g, const EpiArgs& e, int bid, char* smem, 
   if (claim_slot && tid == 0) *claim_slot = claimed;
   FER_STAMP(1);
 
+#ifdef FER_GEMM_EXP
+  // experiments library: static priority instead of the per-segment raise (dbg bit 20: waves 4-7
+  // at priority 1 for the whole main loop; bit 21: waves 0-3)
+  const bool sprio = g.dbg & (3 << 20);
+  if (sprio && ((g.dbg & (1 << 20)) ? wr : !wr)) __builtin_amdgcn_s_setprio(1);
+#else
+  constexpr bool sprio = false;
+#endif
   for (int T = 0; T < nk; ++T) {
     const bool n1 = T + 1 < nk, n2 = T + 2 < nk;
 #pragma unroll
@@ -1393,7 +1401,7 @@ FER_DEV void tile_8ph(const GemmArgs& g, const EpiArgs& e, int bid, char* smem, 
       (void)dummy;
       const int qm = (q == 0 || q == 2) ? 0 : 1;
       const int qn = (q == 0 || q == 3) ? 0 : 1;
-      __builtin_amdgcn_s_setprio(1);
+      if (!sprio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int kk = 0; kk < KS; ++kk)
 #pragma unroll
@@ -1401,13 +1409,14 @@ FER_DEV void tile_8ph(const GemmArgs& g, const EpiArgs& e, int bid, char* smem, 
 #pragma unroll
           for (int i = 0; i < QI; ++i)
             acc[qn * QI + i][qm * QJ + j] = mfma<MT>(fb[qn][kk][i], fa[qm][kk][j], acc[qn * QI + i][qm * QJ + j]);
-      __builtin_amdgcn_s_setprio(0);
+      if (!sprio) __builtin_amdgcn_s_setprio(0);
       __builtin_amdgcn_sched_barrier(0);
       if (T < 16) FER_STAMP(st_i + 3);
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
     }
   }
+  if (sprio) __builtin_amdgcn_s_setprio(0);
   if (nk > 0 && !wr) __builtin_amdgcn_s_barrier();  // waves 0-3 catch up with the stagger
   FER_STAMP(2);
   if (g.dbg & 4) {  // timing experiment: no epilogue (keep the MFMAs alive)
@@ -1689,7 +1698,7 @@ static int launch_bf16(GemmArgs g, const EpiArgs& e, hipStream_t st) {
   hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, WM, WN, AKC, BKC, MT, K>), grid, dim3(64 * WM * WN), 0, st, g, e)
   // the 128^2 K-contiguous MT16 kernel (the small-grid configs: w+ latents, 48 px) also gets the
   // fixed-flag epilogues (row operands through its LDS-DMA staging: the LDS-DMA kinds)
-  if constexpr (BM == 128 && BN == 128 && AKC && BKC && MT == 16) {
+  if constexpr (BM == 128 && (BN == 128 || BN == 64) && AKC && BKC && MT == 16) {
     static const bool gen_only = getenv("FERVIT_EPI_GENERIC") != nullptr;
     int ek = (g.partial || gen_only) ? EPI_GEN : epi_kind(e);
     if (ek == EPI_RES2) ek = EPI_RES;
@@ -1780,6 +1789,20 @@ extern "C" int fer_debug_gemm_ep_stamps(unsigned long long* host) {
 }
 #endif
 
+// Round fill of a grid: tiles / (rounds x slots), slots = CUs x workgroups per CU (128^2: 2 by LDS,
+// 128x64: 3). The 128x64 tiles win where they fill the rounds clearly better (by 0.15 at short K,
+// where their extra per-tile prologue / epilogue weighs more).
+static bool use_128x64(long t128, long t64, int K) {
+  static const int ncu = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      n = 256;
+    return n > 0 ? n : 256;
+  }();
+  auto fill = [](long t, long slots) { return (double)t / (double)(((t + slots - 1) / slots) * slots); };
+  return fill(t64, 3L * ncu) > fill(t128, 2L * ncu) + (K < 1024 ? 0.15 : 0.0);
+}
+
 static int g_forced_cfg = -2;  // -2: read FERVIT_GEMM_CFG once; -1: automatic
 
 static int forced_cfg() {
@@ -1792,7 +1815,7 @@ static int forced_cfg() {
 
 // Tile configuration: 0..3 double-buffered (256^2 MT32, 256^2 MT16, 128^2 MT32, 128^2 MT16),
 // 4..7 BK=32 ring (same order), 8/9 the 8-phase 256^2 kernel (MT16 / MT32), 10 the ping-pong
-// 256x128 kernel (two workgroups per CU).
+// 256x128 kernel (two workgroups per CU), 11 double-buffered 128x64 MT16.
 static bool cfg_is_256(int c) { return c == 0 || c == 1 || c == 4 || c == 5 || c == 8 || c == 9 || c == 10; }
 
 template <bool AKC, bool BKC>
@@ -1808,6 +1831,9 @@ static int dispatch_tile(int cfg, GemmArgs g, const EpiArgs& e, hipStream_t st) 
     case 7: return launch_ring<128, 128, 2, 2, AKC, BKC, 16>(g, e, st);
     case 9: return launch_8ph<AKC, BKC, 32>(g, e, st);
     case 10: return launch_pp<AKC, BKC>(g, e, st);
+    case 11:  // (the MN-contiguous image swizzle needs >= 128-wide tiles: an MN B operand keeps 128^2)
+      if constexpr (BKC) return launch_bf16<128, 64, 2, 2, AKC, BKC, 16>(g, e, st);
+      else return launch_bf16<128, 128, 2, 2, AKC, BKC, 16>(g, e, st);
     default: return launch_8ph<AKC, BKC, 16>(g, e, st);
   }
 }
@@ -1880,6 +1906,11 @@ int gemm_launch(const GemmDesc& d, const EpiArgs& e_in, hipStream_t st) {
   if (cfg < 0) {
     if (d.K >= 8192 || t256 >= 256)  // big grids, and token-long weight gradients (split-K fills the GPU)
       cfg = t256 * splits_for(t256, tgt256) >= 128 ? (!d.a_kc && !d.b_kc ? 5 : 8) : 3;
+    else if (d.a_kc && d.b_kc && t128 >= 128 && use_128x64(t128, (long)((d.M + 127) / 128) * ((d.N + 63) / 64), d.K))
+      // 128x64 tiles (three workgroups per CU) where they fill the rounds better: latent fc2 fwd /
+      // fc1 dgrad (152 tiles of 128^2, K 2048) 28.5 / 27.4 -> 25.4 / 24.3 us, fc1 fwd (608 tiles)
+      // 27.4 -> 24.4 us; qkv fwd (456 tiles, 0.89 of a 128^2 round) stays (15.0 vs 17.6 us)
+      cfg = 11;
     else  // fewer 256^2 tiles than CUs (latent / 48 px configs): 128^2 tiles, two workgroups per CU
       cfg = 3;
   }
@@ -2022,7 +2053,7 @@ extern "C" int64_t fer_gemm_colsum_ws(int M, int N) {
 }
 
 extern "C" int fer_gemm_set_config(int cfg) {
-  if (cfg < -1 || cfg > 10) return fer::set_error("gemm_set_config: cfg must be -1 (automatic) or 0..10");
+  if (cfg < -1 || cfg > 11) return fer::set_error("gemm_set_config: cfg must be -1 (automatic) or 0..11");
   fer::g_forced_cfg = cfg;
   return 0;
 }

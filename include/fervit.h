@@ -97,7 +97,7 @@ int64_t fer_wgrad_group_ws(const fer_wgrad_item* items, int n, int splits);
 int64_t fer_gemm_colsum_ws(int M, int N);
 
 /* Tuning/testing hook (no reference counterpart): force the bf16 GEMM tile configuration for
- * every later fer_gemm call of the process. -1 = automatic (default); 0..10 = fixed kernel
+ * every later fer_gemm call of the process. -1 = automatic (default); 0..11 = fixed kernel
  * (see csrc/gemm.hip dispatch_tile). Results are identical up to fp32 summation order. */
 int fer_gemm_set_config(int cfg);
 

@@ -92,7 +92,7 @@ def test_gemm_persistent_many_tiles(M, N, K):
     assert torch.equal(yd != 0, keep)
 
 
-@pytest.mark.parametrize("cfg", list(range(11)))
+@pytest.mark.parametrize("cfg", list(range(12)))
 def test_gemm_every_tile_config(cfg):
     """Each bf16 kernel configuration (forced through fer_gemm_set_config) on ragged shapes,
     all three operand layouts, split-K, and the fused epilogue."""
@@ -180,11 +180,11 @@ def test_gemm_pre_gate_and_mul(act, dtype, p):
     assert rel_err(cs.cpu(), ref.sum(0)) < 2 * tol
 
 
-@pytest.mark.parametrize("cfg", [8, 3])
+@pytest.mark.parametrize("cfg", [8, 3, 11])
 @pytest.mark.parametrize("p", [0.0, 0.1])
 def test_gemm_8phase_epilogue_kinds(p, cfg):
     """The 8-phase kernel's fixed-flag epilogues (csrc/gemm.hip epi_kind: EPI_STORE, EPI_GATE,
-    EPI_RES2, EPI_MUL2; and the 128^2 kernel's, cfg 3), forced through fer_gemm_set_config on a ragged shape (partial last
+    EPI_RES2, EPI_MUL2; and the 128^2 / 128x64 kernels', cfg 3 / 11), forced through fer_gemm_set_config on a ragged shape (partial last
     tile row and column, K tail): the calls the post-norm layer makes (fervit/layers.py
     PostNormLayerFn), each against an fp32 torch reference with the host-rebuilt keep mask."""
     from fervit._lib import lib
