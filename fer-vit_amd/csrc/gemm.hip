@@ -354,14 +354,14 @@ FER_DEV void epi4(const EpiArgs& e, long m, long n, f32x4 v, uint64_t seed) {
 // ------------------------------------------------------------ tile scheduling
 // XCD-aware, bijective remap (blocks b and b+8 share an XCD under round-robin
 // dispatch) followed by GROUP_M-row grouping for L2 reuse of both panels.
-FER_DEV void tile_of(int bid, int tiles_m, int tiles_n, int& tm, int& tn) {
+FER_DEV void tile_of(int bid, int tiles_m, int tiles_n, int& tm, int& tn, int group = 8) {
   const int nwg = tiles_m * tiles_n;
   int wgid = bid;
   if (nwg >= 16) {
     const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
     wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
   }
-  constexpr int GROUP = 8;
+  const int GROUP = group;
   const int per_group = GROUP * tiles_n;
   const int g = wgid / per_group;
   const int first = g * GROUP;
@@ -1309,7 +1309,15 @@ FER_DEV void tile_8ph(const GemmArgs& g, const EpiArgs& e, int bid, char* smem, 
   FER_STAMP(0);
 
   int tm, tn;
+#ifdef FER_GEMM_EXP
+  // experiments library: row-group size of the tile order (dbg bits 22-23: 8, 4, 16, 32)
+  {
+    const int gs = (g.dbg >> 22) & 3;
+    tile_of(bid, g.tiles_m, g.tiles_n, tm, tn, gs == 0 ? 8 : (gs == 1 ? 4 : (gs == 2 ? 16 : 32)));
+  }
+#else
   tile_of(bid, g.tiles_m, g.tiles_n, tm, tn);
+#endif
   const int m0 = tm * 256, n0 = tn * 256;
   const int ks = blockIdx.y;
   const int kbeg = ks * g.k_chunk;

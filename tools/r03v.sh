@@ -1,0 +1,6 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
+for v in "" "FERVIT_WGRAD_STREAM=0" "FERVIT_FIXED_STRIDE=1" ""; do
+  env $v timeout -k 10 300 python -u bench.py --steps 40 --warmup 10 --no-cpu-baseline --no-traffic --probe-steps 1 > gpurun_out/r03v.txt 2>&1 || { tail -5 gpurun_out/r03v.txt; exit 1; }
+  echo "[$v] $(tail -1 gpurun_out/r03v.txt | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_step"], d["step_ms_median"])')"
+done
