@@ -1910,10 +1910,16 @@ int gemm_launch(const GemmDesc& d, const EpiArgs& e_in, hipStream_t st) {
   static const long tgt128 = getenv("FERVIT_GEMM_SPLIT_T128") ? atol(getenv("FERVIT_GEMM_SPLIT_T128")) : 512;
   static const bool t128_env = getenv("FERVIT_GEMM_SPLIT_T128") != nullptr;
   const long tgt128k = t128_env ? tgt128 : ((d.a_kc && d.b_kc) ? 256 : 512);
+  static const bool wg_mt32 = getenv("FERVIT_WGRAD_MT32") != nullptr;  // A/B switch, see below
   int cfg = forced_cfg();
   if (cfg < 0) {
     if (d.K >= 8192 || t256 >= 256)  // big grids, and token-long weight gradients (split-K fills the GPU)
-      cfg = t256 * splits_for(t256, tgt256) >= 128 ? (!d.a_kc && !d.b_kc ? 5 : 8) : 3;
+      // (MN x MN weight gradients split >= 16 ways -- out_proj / patch embed, 9 tiles x 28 splits --
+      // run 97.7 -> 74.1 us alone on the MT32 ring, but the ViT-B step got 0.1-0.3 ms SLOWER with
+      // it on the weight-gradient stream (profiles/r03x_*, r03z_*): opt-in, FERVIT_WGRAD_MT32=1)
+      cfg = t256 * splits_for(t256, tgt256) >= 128
+                ? (!d.a_kc && !d.b_kc ? (splits_for(t256, tgt256) >= 16 && wg_mt32 ? 4 : 5) : 8)
+                : 3;
     else if (d.a_kc && d.b_kc && t128 >= 128 && use_128x64(t128, (long)((d.M + 127) / 128) * ((d.N + 63) / 64), d.K))
       // 128x64 tiles (three workgroups per CU) where they fill the rounds better: latent fc2 fwd /
       // fc1 dgrad (152 tiles of 128^2, K 2048) 28.5 / 27.4 -> 25.4 / 24.3 us, fc1 fwd (608 tiles)

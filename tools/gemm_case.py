@@ -29,6 +29,7 @@ def make_cases(dev="cuda"):
     dq = r(M, 3 * D)
     cs = torch.zeros(F, device=dev)
     gw = torch.zeros(F, D, device=dev)
+    gwo, gwq = torch.zeros(D, D, device=dev), torch.zeros(3 * D, D, device=dev)
     p = 0.1
     return {
         # name: (launch, flop)
@@ -43,6 +44,8 @@ def make_cases(dev="cuda"):
         "store_outd": (lambda: ops.linear_fwd(x, wo, out=out_d), 2 * M * D * D),
         "plain_fc1": (lambda: ops.linear_fwd(x, w1, out=out_f), 2 * M * F * D),
         "wgrad": (lambda: ops.linear_wgrad(dF, x, gw), 2 * M * F * D),
+        "wgrad_out": (lambda: ops.linear_wgrad(x, x, gwo), 2 * M * D * D),
+        "wgrad_qkv": (lambda: ops.linear_wgrad(dq, x, gwq), 2 * M * 3 * D * D),
     }
 
 
