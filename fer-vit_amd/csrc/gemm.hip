@@ -1904,7 +1904,11 @@ int gemm_launch(const GemmDesc& d, const EpiArgs& e_in, hipStream_t st) {
   };
   // split targets (workgroups per launch) of the 256^2 / 128^2 tile configs; FERVIT_GEMM_SPLIT_T256 /
   // FERVIT_GEMM_SPLIT_T128 override them (tuning runs only)
+  // (MN x MN weight gradients: 192 workgroups, not one per CU -- they run beside the compute stream,
+  // and leaving it CUs took the ViT-B step 36.06-36.33 -> 35.81-36.02 ms; 128 is 39 ms: the last
+  // layers' weight gradients then form a long tail; profiles/r03aa_wgrad_split_target_ab.txt)
   static const long tgt256 = getenv("FERVIT_GEMM_SPLIT_T256") ? atol(getenv("FERVIT_GEMM_SPLIT_T256")) : 256;
+  static const long tgt256_mn = getenv("FERVIT_GEMM_SPLIT_T256") ? tgt256 : 192;
   // (128^2, K-contiguous: split only below half a round; the ordered slab reduction costs more than the
   // idle CUs of an unsplit 152-228 tile grid -- latent fc2 fwd 50.7 -> 29.4 us, qkv dgrad 46.4 -> 22.9 us)
   static const long tgt128 = getenv("FERVIT_GEMM_SPLIT_T128") ? atol(getenv("FERVIT_GEMM_SPLIT_T128")) : 512;
@@ -1918,7 +1922,7 @@ int gemm_launch(const GemmDesc& d, const EpiArgs& e_in, hipStream_t st) {
       // run 97.7 -> 74.1 us alone on the MT32 ring, but the ViT-B step got 0.1-0.3 ms SLOWER with
       // it on the weight-gradient stream (profiles/r03x_*, r03z_*): opt-in, FERVIT_WGRAD_MT32=1)
       cfg = t256 * splits_for(t256, tgt256) >= 128
-                ? (!d.a_kc && !d.b_kc ? (splits_for(t256, tgt256) >= 16 && wg_mt32 ? 4 : 5) : 8)
+                ? (!d.a_kc && !d.b_kc ? (splits_for(t256, tgt256_mn) >= 16 && wg_mt32 ? 4 : 5) : 8)
                 : 3;
     else if (d.a_kc && d.b_kc && t128 >= 128 && use_128x64(t128, (long)((d.M + 127) / 128) * ((d.N + 63) / 64), d.K))
       // 128x64 tiles (three workgroups per CU) where they fill the rounds better: latent fc2 fwd /
@@ -1928,7 +1932,7 @@ int gemm_launch(const GemmDesc& d, const EpiArgs& e_in, hipStream_t st) {
     else  // fewer 256^2 tiles than CUs (latent / 48 px configs): 128^2 tiles, two workgroups per CU
       cfg = 3;
   }
-  int splits = cfg_is_256(cfg) ? splits_for(t256, tgt256) : splits_for(t128, tgt128k);
+  int splits = cfg_is_256(cfg) ? splits_for(t256, (!d.a_kc && !d.b_kc) ? tgt256_mn : tgt256) : splits_for(t128, tgt128k);
   g.splits = splits;
   g.k_chunk = splits > 1 ? (((d.K + splits - 1) / splits + BK - 1) / BK) * BK : d.K;
   if (splits > 1) g.splits = (d.K + g.k_chunk - 1) / g.k_chunk;
