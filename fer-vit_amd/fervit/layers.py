@@ -88,6 +88,9 @@ def _wgrad(dy, x, out, **kw):
 # each: the w+ latent (4,864 rows) and 48 px (640) configurations. ViT-B/16 (50,432 rows) keeps
 # the per-weight split-K launches, issued as soon as each dY exists.
 WGRAD_GROUP_MAX_M = int(os.environ.get("FERVIT_WGRAD_GROUP_MAX_M", "16384"))
+# A/B: issue each weight gradient after the input-gradient GEMM that shares its dY instead of
+# before it (the weight-gradient stream then overlaps the next kernels of the chain)
+WGRAD_LATE = os.environ.get("FERVIT_WGRAD_LATE") == "1"
 
 
 class _WgradBatch:
@@ -168,24 +171,37 @@ class PostNormLayerFn(torch.autograd.Function):
         ops.layernorm_bwd(dout, z, m2, r2, n2w.data, dx=dz, dx_drop=dh2, dropout=pd, seed=seeds[3], dgamma=gn2w,
                           dbeta=gn2b, dbias=gb2, accumulate=acc)
         dh2 = dz if dh2 is None else dh2
-        wb.add(dh2, g, gw2, acc)
+        late = WGRAD_LATE
+        if not late:
+            wb.add(dh2, g, gw2, acc)
         # linear1.bias grad = column sums of dF, fused into this GEMM's epilogue
         dF = _dgrad(flat, dh2, w2, dt, aux=f, aux_act="mul", colsum=gb1, colsum_accumulate=acc)
-        wb.add(dF, x1, gw1, acc)
+        if late:
+            wb.add(dh2, g, gw2, acc)
+        else:
+            wb.add(dF, x1, gw1, acc)
         dx1 = _dgrad(flat, dF, w1, dt, res=dz)
+        if late:
+            wb.add(dF, x1, gw1, acc)
         # LN1 (+ dropout of the attention branch, + out_proj bias grad)
         dy = torch.empty_like(y)
         dhh = torch.empty_like(y) if pd > 0 else None
         ops.layernorm_bwd(dx1, y, m1, r1, n1w.data, dx=dy, dx_drop=dhh, dropout=pd, seed=seeds[1], dgamma=gn1w,
                           dbeta=gn1b, dbias=gout_b, accumulate=acc)
         dhh = dy if dhh is None else dhh
-        wb.add(dhh, o, gout_w, acc)
+        if not late:
+            wb.add(dhh, o, gout_w, acc)
         do = _dgrad(flat, dhh, out_w, dt)
+        if late:
+            wb.add(dhh, o, gout_w, acc)
         dqkv = _empty(M, 3 * D, x)
         ops.attention_bwd(qkv, o, do, lse, dqkv, cfg.B, cfg.N, cfg.H, dh, dropout=pd, seed=seeds[0], colsum=gin_b,
                           colsum_accumulate=acc)
-        wb.add(dqkv, x, gin_w, acc)
+        if not late:
+            wb.add(dqkv, x, gin_w, acc)
         dx = _dgrad(flat, dqkv, in_w, dt, res=dy)
+        if late:
+            wb.add(dqkv, x, gin_w, acc)
         wb.flush()
         _finish(flat, P, needs)
         ctx.saved = None
