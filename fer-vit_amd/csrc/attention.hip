@@ -270,12 +270,50 @@ FER_DEV void fwd_load_q(bf16x8 (&qf)[4], const bf16* qkv, long ldq, int unit, in
   }
 }
 
-template <int NB>
+// Keep-bit words of the persistent path, computed ahead of the forward (data-independent: only the
+// seed and the element indices enter). Layout as attn_fwd_pers documents: word ((bh*NB + kb)*NB +
+// qb)*32 + j = bits over the 32 queries of block qb for key kb*32 + j, the same hash of the same
+// element index for every (query, key) -- padding rows / keys included -- so the words are the ones
+// the forward's ballots produced. Thread = (bh, kb, qb, key pair jp): 32 hashes, two words (keys
+// 2jp, 2jp+1 = the two 16-bit halves of one hash), one 8-byte store (16 threads = one 128-byte row).
+// (Opt-in, FERVIT_ATTN_MASK_PRE=1: measured no faster than hashing inside the forward.)
+__global__ __launch_bounds__(256) void attn_mask_gen(uint32_t* __restrict__ mask, int BH, int N, int NB, uint32_t thr,
+                                                     uint64_t seed) {
+  seed = step_seed(seed);
+  const long t = (long)blockIdx.x * 256 + threadIdx.x;
+  const long blk = t >> 4;  // (bh, kb, qb)
+  if (blk >= (long)BH * NB * NB) return;
+  const int jp = (int)(t & 15);
+  const int qb = (int)(blk % NB), kb = (int)((blk / NB) % NB), bh = (int)(blk / ((long)NB * NB));
+  const uint32_t kpair = (uint32_t)(kb * 16 + jp);  // (kb*32 + 2*jp) >> 1
+  const uint32_t thr_hi = thr << 16;
+  uint32_t w0 = 0, w1 = 0;
+#pragma unroll 8
+  for (int i = 0; i < 32; ++i) {
+    const uint32_t h = fer_hash(seed, (drop_row(bh, N, qb * 32 + i) >> 1) + kpair);
+    w0 |= (uint32_t)((h & 0xFFFFu) >= thr) << i;
+    w1 |= (uint32_t)(h >= thr_hi) << i;
+  }
+  *(uint2*)(mask + blk * 32 + 2 * jp) = uint2{w0, w1};
+}
+
+// Dropout of the 16 S^T accumulator registers from precomputed keep words (attn_mask_gen): the
+// 64-bit lane mask of register r is (word of key a) | (word of key a+4) << 32 with a = acc_row(r, 0)
+// -- lane l holds query l & 31 and, in the upper half, key a + 4 -- i.e. exactly the ballot the
+// forward used to take of its keep compares (inverse ballot: one v_cndmask per element with the
+// SGPR pair as its lane mask), the words by scalar loads.
+FER_DEV float keep_sel(float v, uint64_t lanemask) {
+  return __builtin_amdgcn_inverse_ballot_w64(lanemask) ? v : 0.f;
+}
+
+template <int NB, bool PRE = false>
 __global__ __launch_bounds__(64 * (NB + 1)) void attn_fwd_pers(const bf16* __restrict__ qkv, long ldq,
                                                                bf16* __restrict__ out, long ldo,
                                                                float* __restrict__ lse, uint32_t* __restrict__ mask,
                                                                int BH, int N, int H, int dh, float sl2, uint32_t thr,
                                                                float dscale, uint64_t seed, WqArgs wq) {
+  // PRE: the keep words were written by attn_mask_gen; this kernel reads them (scalar loads) instead
+  // of hashing, ballotting and storing them
   seed = step_seed(seed);
   constexpr int IMG = NB * 32 * 128;
   __shared__ __attribute__((aligned(1024))) char lds[4 * IMG + 16];  // 2 x (K image, V image), unit hand-off
@@ -333,6 +371,13 @@ __global__ __launch_bounds__(64 * (NB + 1)) void attn_fwd_pers(const bf16* __res
       for (int s = 0; s < 4; ++s) kfr[s] = rd_row(Ki, lane & 31, 2 * s + hh);
       // softmax + dropout + P.V of key block kb, whose S^T is in st
       auto block = [&](int kb, f32x16& st) {
+        uint32_t kw[32];  // PRE: this block's keep words, loaded (scalar) ahead of the softmax
+        if (PRE) {
+          const __attribute__((address_space(4))) uint32_t* mw =
+              (const __attribute__((address_space(4))) uint32_t*)(mask + (((long)bh * NB + kb) * NB + w) * 32);
+#pragma unroll
+          for (int j = 0; j < 32; ++j) kw[j] = mw[j];
+        }
         bf16x8 vfr[2][2];
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2)
@@ -361,7 +406,13 @@ __global__ __launch_bounds__(64 * (NB + 1)) void attn_fwd_pers(const bf16* __res
           st[r] = ex2(fmaf(st[r], sl2, -m));
           l += st[r];
         }
-        if (thr) {
+        if (PRE) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int a = acc_row(r, 0);
+            st[r] = keep_sel(st[r], (uint64_t)kw[a] | ((uint64_t)kw[a + 4] << 32));
+          }
+        } else if (thr) {
           const uint32_t p0 = (row >> 1) + kb * 16 + 2 * hh;  // hash pair of register 0
           uint64_t bal[16];
 #pragma unroll
@@ -1553,11 +1604,27 @@ extern "C" int fer_attention_fwd(int dtype, const void* qkv, int64_t ld_qkv, voi
 #undef FER_FOCC
     const int grid = std::min(B * H, n_cus() * occ);
     const WqArgs wq = fixed_stride() ? WqArgs{} : wq_prepare_here(st, grid, B * H);
+    // FERVIT_ATTN_MASK_PRE=1: keep words by attn_mask_gen ahead of the forward, which then selects
+    // with them instead of hashing (opt-in: the hashing costs the same VALU time in either kernel --
+    // ViT-B forward 135-138 us inline vs 153-155 us mask kernel + forward, step +0.1-0.3 ms,
+    // profiles/r03ad_attn_mask_pre_ab.txt)
+    static const bool pre_mask = getenv("FERVIT_ATTN_MASK_PRE") != nullptr;
+    const bool pre = mask && pre_mask;
+    if (pre) {
+      const long words = (long)B * H * nb * nb * 32;
+      hipLaunchKernelGGL(attn_mask_gen, dim3((unsigned)ceil_div(words / 2, 256)), dim3(256), 0, st, mask, B * H, N,
+                         nb, drop_thresh, seed);
+    }
 #define FER_FPERS(NBV)                                                                                       \
   case NBV:                                                                                                  \
-    hipLaunchKernelGGL(attn_fwd_pers<NBV>, dim3(grid), dim3(64 * (NBV + 1)), 0, st, (const bf16*)qkv,        \
-                       (long)ld_qkv, (bf16*)out, (long)ld_out, lse, mask, B * H, N, H, dh, sl2, drop_thresh,  \
-                       drop_scale, seed, wq);                                                               \
+    if (pre)                                                                                                 \
+      hipLaunchKernelGGL((attn_fwd_pers<NBV, true>), dim3(grid), dim3(64 * (NBV + 1)), 0, st, (const bf16*)qkv, \
+                         (long)ld_qkv, (bf16*)out, (long)ld_out, lse, mask, B * H, N, H, dh, sl2, drop_thresh, \
+                         drop_scale, seed, wq);                                                             \
+    else                                                                                                     \
+      hipLaunchKernelGGL((attn_fwd_pers<NBV, false>), dim3(grid), dim3(64 * (NBV + 1)), 0, st, (const bf16*)qkv, \
+                         (long)ld_qkv, (bf16*)out, (long)ld_out, lse, mask, B * H, N, H, dh, sl2, drop_thresh, \
+                         drop_scale, seed, wq);                                                             \
     break;
     switch (nb) {
       FER_FPERS(1) FER_FPERS(2) FER_FPERS(3) FER_FPERS(4) FER_FPERS(5) FER_FPERS(6) FER_FPERS(7)
