@@ -79,7 +79,12 @@ def _finish(flat: FlatParams, params, needs) -> None:
 
 
 def _wgrad(dy, x, out, **kw):
-    """dW (+)= dy^T x on the weight-gradient stream (runtime.WGRAD)."""
+    """dW (+)= dy^T x on the weight-gradient stream (runtime.WGRAD) (FERVIT_WGRAD_SINGLE_GROUP=1: a
+    plain one at a small token count as a grouped launch of one, see WGRAD_SINGLE_GROUP)."""
+    if (WGRAD_SINGLE_GROUP and set(kw) <= {"accumulate"} and dy.dtype == torch.bfloat16
+            and out.dtype == torch.float32 and dy.shape[0] <= WGRAD_GROUP_MAX_M):
+        acc = bool(kw.get("accumulate", False))
+        return WGRAD.run(lambda: ops.linear_wgrad_group([(dy, x, out, acc)]), dy, x)
     return WGRAD.run(lambda: ops.linear_wgrad(dy, x, out, **kw), dy, x)
 
 
@@ -88,6 +93,10 @@ def _wgrad(dy, x, out, **kw):
 # each: the w+ latent (4,864 rows) and 48 px (640) configurations. ViT-B/16 (50,432 rows) keeps
 # the per-weight split-K launches, issued as soon as each dY exists.
 WGRAD_GROUP_MAX_M = int(os.environ.get("FERVIT_WGRAD_GROUP_MAX_M", "16384"))
+# A/B, opt-in (FERVIT_WGRAD_SINGLE_GROUP=1): lone weight gradients (input projections, adapters, 48 px
+# patch embed) as groups of one -- measured slower (hybrid 6.52-6.61 -> 6.84-6.88 ms: an adapter's
+# 6-tile gradient gets too few workgroups), profiles/r03af_single_wgrad_group_ab.txt
+WGRAD_SINGLE_GROUP = os.environ.get("FERVIT_WGRAD_SINGLE_GROUP", "0") == "1"
 # A/B: issue each weight gradient after the input-gradient GEMM that shares its dY instead of
 # before it (the weight-gradient stream then overlaps the next kernels of the chain)
 WGRAD_LATE = os.environ.get("FERVIT_WGRAD_LATE") == "1"
