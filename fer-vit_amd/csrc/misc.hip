@@ -654,11 +654,22 @@ __global__ __launch_bounds__(256) void dot_part_kernel(const T* __restrict__ a, 
   __syncthreads();
   if (threadIdx.x == 0) part[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
 }
-__global__ void sum_final_kernel(const float* __restrict__ part, int n, float* out, int accumulate) {
-  if (threadIdx.x) return;
+// Fixed-order (deterministic) sum of the partials: thread t adds partials t, t+256, ... in order,
+// then a butterfly per wave and the four wave sums in order. (One thread walking up to 1024 partials
+// was a chain of dependent L2 loads: 46 us per call, the hybrid adapters' alpha gradients 0.5 ms
+// per step.)
+__global__ __launch_bounds__(256) void sum_final_kernel(const float* __restrict__ part, int n, float* out,
+                                                        int accumulate) {
+  __shared__ float red[4];
   float s = 0.f;
-  for (int i = 0; i < n; ++i) s += part[i];
-  *out = accumulate ? *out + s : s;
+  for (int i = threadIdx.x; i < n; i += 256) s += part[i];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float t = (red[0] + red[1]) + (red[2] + red[3]);
+    *out = accumulate ? *out + t : t;
+  }
 }
 template <typename T>
 __global__ void dropout_kernel(const T* __restrict__ x, T* __restrict__ y, long n, uint32_t thr, float sc,
@@ -1059,7 +1070,7 @@ extern "C" int fer_dot(int dtype, const void* a, const void* b, int64_t n, float
   else
     hipLaunchKernelGGL(dot_part_kernel<float>, dim3(nb), dim3(256), 0, st, (const float*)a, (const float*)b, (long)n,
                        ws);
-  hipLaunchKernelGGL(sum_final_kernel, dim3(1), dim3(64), 0, st, ws, nb, out, accumulate);
+  hipLaunchKernelGGL(sum_final_kernel, dim3(1), dim3(256), 0, st, ws, nb, out, accumulate);
   return hip_check("dot");
 }
 extern "C" int fer_sumsq(const float* x, int64_t n, float* out, float* ws, int64_t ws_bytes, fer_stream_t stream) {

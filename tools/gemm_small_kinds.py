@@ -18,6 +18,8 @@ def main():
     r = lambda *s: torch.randn(*s, device="cuda", generator=g).to(torch.bfloat16)
     x, h = r(M, D), r(M, F)
     wqkv, wo, w1, w2, w2t = r(3 * D, D), r(D, D), r(F, D), r(D, F), r(F, D)
+    w1t, wqt = r(D, F), r(D, 3 * D)
+    dq = r(M, 3 * D)
     bq, bo, b1, b2 = (torch.zeros(n, device="cuda") for n in (3 * D, D, F, D))
     gate = torch.empty(M, F, device="cuda", dtype=torch.bfloat16)
     cs = torch.zeros(F, device="cuda")
@@ -28,6 +30,10 @@ def main():
                                                   drop_ld=F), 2 * M * F * D),
         "fc2 fwd (res+drop)": (lambda: ops.linear_fwd(h, w2, b2, res=x, dropout=0.1, seed=7, drop_ld=D), 2 * M * F * D),
         "fc2 dgrad (mul+cs)": (lambda: ops.linear_fwd(x, w2t, aux=gate, aux_act="mul", colsum=cs), 2 * M * F * D),
+        # the frozen trunk's input gradients (timm pre-norm block: no epilogue)
+        "fc1 dgrad (store)": (lambda: ops.linear_fwd(h, w1t), 2 * M * F * D),
+        "proj dgrad (store)": (lambda: ops.linear_fwd(x, wo), 2 * M * D * D),
+        "qkv dgrad (store)": (lambda: ops.linear_fwd(dq, wqt), 2 * M * 3 * D * D),
     }
     tot = 0.0
     for k, (fn, fl) in cases.items():
