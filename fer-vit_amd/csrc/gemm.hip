@@ -1747,8 +1747,10 @@ static int launch_8ph(GemmArgs g, const EpiArgs& e, hipStream_t st) {
     return n > 0 ? n : 256;
   }();
   static const bool persist = getenv("FERVIT_GEMM_NOPERSIST") == nullptr;  // A/B switch
+  // FERVIT_GEMM_PERSIST_WG: persistent grid size (tuning runs; default one workgroup per CU)
+  static const int pwg = getenv("FERVIT_GEMM_PERSIST_WG") ? atoi(getenv("FERVIT_GEMM_PERSIST_WG")) : ncu;
   const int ntiles = g.tiles_m * g.tiles_n;
-  const int gx = persist ? std::min(ntiles, std::max(8, ncu / 8 * 8)) : ntiles;
+  const int gx = persist ? std::min(ntiles, std::max(8, pwg / 8 * 8)) : ntiles;
   g.tq = nullptr;
   WqArgs w{};
   if (persist && !fixed_stride_mode() && g.splits == 1) {
