@@ -562,9 +562,15 @@ FER_DEV void tile_epilogue(const GemmArgs& g, const EpiArgs& e, AccT (&acc)[FN][
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's partial is out
       __syncthreads();  // every wave's partial is out; every wave is past the main loop's LDS reads
       volatile unsigned* flag = (volatile unsigned*)smem;
-      if (tid_ == 0)
-        *flag = __hip_atomic_fetch_add(g.cnt + (m0 / BM) + (n0 / BN) * g.tiles_m, 1u, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
+      if (tid_ == 0) {  // acquire after the last ticket, as in gemm_wgrad_group_kernel
+        const unsigned tk = __hip_atomic_fetch_add(g.cnt + (m0 / BM) + (n0 / BN) * g.tiles_m, 1u, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT);
+        if (tk == (unsigned)(g.splits - 1)) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        *flag = tk;
+      }
       __syncthreads();
       const bool last = *flag == (unsigned)(g.splits - 1);
       __syncthreads();  // the flag word is read before any later use of the LDS (persistent kernels)
@@ -1666,8 +1672,18 @@ __global__ __launch_bounds__(128 * WN, 1) void gemm_wgrad_group_kernel(WgGroup g
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drained
     __syncthreads();
     volatile unsigned* flag = (volatile unsigned*)(smem + NST * STAGE);
-    if (threadIdx.x == 0)
-      *flag = __hip_atomic_fetch_add(grp.cnt + tl, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) {
+      // the sc1 stores are write-through and drained: no release needed (MI355X_MICROARCH.md). The
+      // last split also takes an agent-scope acquire before its sc1 loads: the sc1-only hand-off
+      // is measured at one workgroup per CU, this kernel runs two (a release on every producer
+      // measured +5 us per launch and is not needed for write-through stores).
+      const unsigned tk = __hip_atomic_fetch_add(grp.cnt + tl, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (tk == (unsigned)(S - 1)) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      *flag = tk;
+    }
     __syncthreads();
     if (*flag != (unsigned)(S - 1)) return;  // not the last split of this tile
     // last split: slabs in split order (sc1 loads: every load of the handed-off bytes)
