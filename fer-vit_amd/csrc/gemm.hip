@@ -1322,7 +1322,9 @@ FER_DEV void tile_8ph(const GemmArgs& g, const EpiArgs& e, int bid, char* smem, 
     tile_of(bid, g.tiles_m, g.tiles_n, tm, tn, gs == 0 ? 8 : (gs == 1 ? 4 : (gs == 2 ? 16 : 32)));
   }
 #else
-  tile_of(bid, g.tiles_m, g.tiles_n, tm, tn);
+  // GELU-gate fc1 forward: row groups of 4 tiles (377 -> 367-370 us alone, profiles/r03w_tile_group_ab.txt;
+  // the other kinds gain nothing from it); g.dbg bit 24 (FERVIT_GEMM_DBG) keeps 8 (A/B)
+  tile_of(bid, g.tiles_m, g.tiles_n, tm, tn, (EK == EPI_GATE && !(g.dbg & (1 << 24))) ? 4 : 8);
 #endif
   const int m0 = tm * 256, n0 = tn * 256;
   const int ks = blockIdx.y;
