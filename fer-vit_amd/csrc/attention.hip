@@ -1690,6 +1690,7 @@ extern "C" int fer_attention_bwd(int dtype, const void* qkv, int64_t ld_qkv, con
   static const bool old_bwd = getenv("FERVIT_ATTN_BWD_OLD") != nullptr;  // A/B switch (p = 0 only)
   if (pers_path(dtype, N, dh) && !general && !(old_bwd && !drop_thresh)) {
     const uint32_t* mask = drop_thresh ? (const uint32_t*)(lse + lse_floats(B, N, H)) : nullptr;
+    if (colsum) ws = reduction_ws(ws, (size_t)B * nb * D3 * 4, D3, st);
     int occ = 1;
 #define FER_BOCC(NBV)                                                               \
   case NBV: {                                                                       \
@@ -1718,6 +1719,7 @@ extern "C" int fer_attention_bwd(int dtype, const void* qkv, int64_t ld_qkv, con
     return hip_check("attention_bwd_colsum");
   }
   if (nb <= 8 && dh <= 64 && !general) {
+    if (colsum) ws = reduction_ws(ws, (size_t)B * D3 * 4, D3, st);
 #define FER_FUSED(NBV)                                                                                       \
   case NBV:                                                                                                  \
     hipLaunchKernelGGL(attn_bwd_fused_bf16<NBV>, dim3(B * H), dim3(64 * NBV), 0, st, (const bf16*)qkv,       \

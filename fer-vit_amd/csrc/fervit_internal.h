@@ -41,6 +41,9 @@ inline int ceil_div(long a, long b);
 // out_k[c % seg] (+)= scale * sum_b part[b*ld + c]  (deterministic, misc.hip)
 void part_reduce(const float* part, int nb, long ld, int ncols, int seg, float* o0, float* o1, float* o2,
                  int accumulate, const float* scale, hipStream_t st);
+// Workspace for column partials that part_reduce will sum: inside fer_reduce_defer's window (same
+// stream, a shape the batched reduction takes) a slice of the deferral arena, else ws itself (misc.hip)
+float* reduction_ws(float* ws, size_t bytes, int ncols, hipStream_t st);
 
 inline int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
 

@@ -1958,7 +1958,9 @@ int gemm_launch(const GemmDesc& d, const EpiArgs& e_in, hipStream_t st) {
   if (splits > 1) g.splits = (d.K + g.k_chunk - 1) / g.k_chunk;
   g.partial = g.splits > 1;
   g.ws = d.ws;
-  g.cs_part = e.colsum ? d.ws : nullptr;
+  g.cs_part = e.colsum ? reduction_ws(d.ws, (size_t)((d.M + (cfg_is_256(cfg) ? 255 : 127)) / (cfg_is_256(cfg) ? 256 : 128)) * d.N * 4,
+                                      d.N, st)
+                       : nullptr;
   g.cnt = nullptr;
   // in-launch split-K reduction (tile_epilogue; tickets after the slabs in the workspace, zeroed
   // here) only with FERVIT_SPLITK_INLAUNCH=1: measured slower than the separate full-chip
@@ -1983,8 +1985,8 @@ int gemm_launch(const GemmDesc& d, const EpiArgs& e_in, hipStream_t st) {
   int rc = hip_check("gemm_bf16");
   if (!rc && e.colsum) {  // fixed-order reduction of the per-tile column partials
     const int bm = cfg_is_256(cfg) ? 256 : 128;
-    part_reduce(d.ws, (d.M + bm - 1) / bm, d.N, d.N, d.N, e.colsum, nullptr, nullptr, e.colsum_accumulate, nullptr,
-                st);
+    part_reduce(g.cs_part, (d.M + bm - 1) / bm, d.N, d.N, d.N, e.colsum, nullptr, nullptr, e.colsum_accumulate,
+                nullptr, st);
     rc = hip_check("gemm_colsum_reduce");
   }
   if (rc || !g.partial || g.cnt) return rc;

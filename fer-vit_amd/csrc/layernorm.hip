@@ -452,6 +452,7 @@ extern "C" int fer_layernorm_bwd(int dtype, const void* dy, int64_t lddy, const 
   const int nblk = ln_bwd_blocks(M);
   if (want && (!ws || ws_bytes < fer_layernorm_bwd_ws(M, D))) return set_error("layernorm_bwd: workspace too small");
   hipStream_t st = (hipStream_t)stream;
+  if (want) ws = reduction_ws(ws, (size_t)fer_layernorm_bwd_ws(M, D), 3 * D, st);
   static const bool old_ln = getenv("FERVIT_LN_OLD") != nullptr;  // A/B switch
   if (dtype == FER_BF16 && D % 8 == 0 && lddy % 8 == 0 && ldx % 8 == 0 && lddx % 8 == 0 && (!res || ldr % 8 == 0) &&
       !old_ln) {

@@ -17,13 +17,13 @@ namespace fer {
 // that the grid covers the CUs (ViT-B: 2304 columns -> 288 blocks of 8 columns instead of 72 of
 // 32). Fixed association order for a given shape -> deterministic.
 template <int CB>
-__global__ __launch_bounds__(256) void part_reduce_kernel(const float* __restrict__ part, int nb, long ld, int ncols,
-                                                          int seg, float* o0, float* o1, float* o2, int accumulate,
-                                                          const float* __restrict__ scale) {
+__device__ __forceinline__ void part_reduce_body(const float* __restrict__ part, int nb, long ld, int ncols, int seg,
+                                                 float* o0, float* o1, float* o2, int accumulate,
+                                                 const float* __restrict__ scale, int bx) {
   constexpr int RP = 256 / CB;
   __shared__ float red[RP][CB + 1];
   const int cx = threadIdx.x % CB, j = threadIdx.x / CB;
-  const int c = blockIdx.x * CB + cx;
+  const int c = bx * CB + cx;
   float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if (c < ncols) {
     int b = j;
@@ -45,14 +45,95 @@ __global__ __launch_bounds__(256) void part_reduce_kernel(const float* __restric
     if (o) o[col] = accumulate ? o[col] + t : t;
   }
 }
+template <int CB>
+__global__ __launch_bounds__(256) void part_reduce_kernel(const float* __restrict__ part, int nb, long ld, int ncols,
+                                                          int seg, float* o0, float* o1, float* o2, int accumulate,
+                                                          const float* __restrict__ scale) {
+  part_reduce_body<CB>(part, nb, ld, ncols, seg, o0, o1, o2, accumulate, scale, blockIdx.x);
+}
+
+// Deferred reductions (fer_reduce_defer): inside a backward pass the column partials of the bias /
+// LayerNorm / attention-bias gradients are written into an arena instead of the shared scratch and
+// their part_reduce launches are queued; fer_reduce_flush (the end of the backward, or before a
+// gradient-ready hook such as the DDP bucket all-reduce reads them) runs them all as ONE launch.
+// Same per-column arithmetic as part_reduce_kernel<8> (the batch only takes shapes that would use
+// the 8-column kernel), so bit-identical results; only their time on the compute stream moves.
+struct RedDesc {
+  const float* part;
+  long ld;
+  float* o[3];
+  int nb, ncols, seg, accumulate, blk0;
+};
+constexpr int kRedMax = 56;  // kernel-argument budget (64 bytes each)
+struct RedBatch {
+  RedDesc d[kRedMax];
+  int n;
+};
+__global__ __launch_bounds__(256) void part_reduce_multi_kernel(const RedBatch b) {
+  int i = 0;
+  while (i + 1 < b.n && (int)blockIdx.x >= b.d[i + 1].blk0) ++i;
+  const RedDesc& d = b.d[i];
+  part_reduce_body<8>(d.part, d.nb, d.ld, d.ncols, d.seg, d.o[0], d.o[1], d.o[2], d.accumulate, nullptr,
+                      blockIdx.x - d.blk0);
+}
+static struct {
+  bool on = false, take = false;  // window open (queue valid) / taking new reductions
+  char* arena = nullptr;
+  size_t cap = 0, used = 0;
+  hipStream_t st = nullptr;
+  RedBatch b;
+  int blocks = 0;
+} g_red;
+static bool red_batchable(int ncols) { return ceil_div(ncols, 16) < 256; }
+static int red_flush() {
+  if (g_red.b.n) {
+    hipLaunchKernelGGL(part_reduce_multi_kernel, dim3(g_red.blocks), dim3(256), 0, g_red.st, g_red.b);
+    g_red.b.n = 0;
+    g_red.blocks = 0;
+  }
+  g_red.used = 0;
+  return hip_check("reduce_flush");
+}
+// Only partial sets up to FERVIT_REDUCE_MAX_KB (default 2 MB) are deferred: the small-token
+// configurations' (latent w+ 1.5-1.9 MB per LayerNorm / attention bias) gain one launch each
+// (latent ViT 2.22 -> 2.16 ms), while ViT-B's (4.7-16.5 MB, 52 per step) measured 35.62 -> 35.75
+// ms deferred (their sums then re-read from HBM at the end of the backward instead of from the
+// last-level cache right after the producer; profiles/r03am_reduce_defer_ab.txt).
+float* reduction_ws(float* ws, size_t bytes, int ncols, hipStream_t st) {
+  static const size_t max_b = (getenv("FERVIT_REDUCE_MAX_KB") ? atol(getenv("FERVIT_REDUCE_MAX_KB")) : 2048) * 1024L;
+  if (!g_red.take || st != g_red.st || !red_batchable(ncols) || bytes > g_red.cap || bytes > max_b) return ws;
+  bytes = (bytes + 255) & ~(size_t)255;
+  if (g_red.used + bytes > g_red.cap || g_red.b.n == kRedMax) red_flush();
+  float* p = (float*)(g_red.arena + g_red.used);
+  g_red.used += bytes;
+  return p;
+}
+
 void part_reduce(const float* part, int nb, long ld, int ncols, int seg, float* o0, float* o1, float* o2,
                  int accumulate, const float* scale, hipStream_t st) {
+  const bool in_arena = g_red.take && st == g_red.st && (const char*)part >= g_red.arena &&
+                        (const char*)part < g_red.arena + g_red.cap;
+  bool dup = false;  // an output already queued: keep the two updates in stream order
+  for (int i = 0; i < g_red.b.n && !dup; ++i)
+    for (int k = 0; k < 3; ++k)
+      for (float* o : {o0, o1, o2}) dup |= o && g_red.b.d[i].o[k] == o;
+  if (in_arena && !scale && red_batchable(ncols) && g_red.b.n < kRedMax && !dup) {
+    g_red.b.d[g_red.b.n++] = RedDesc{part, ld, {o0, o1, o2}, nb, ncols, seg, accumulate, g_red.blocks};
+    g_red.blocks += ceil_div(ncols, 8);
+    return;
+  }
+  if (g_red.b.n && (in_arena || dup)) {  // run the queue first; this call's partials stay valid
+    const size_t keep = g_red.used;
+    red_flush();
+    g_red.used = keep;
+  }
   if (ceil_div(ncols, 16) >= 256)
     hipLaunchKernelGGL(part_reduce_kernel<16>, dim3(ceil_div(ncols, 16)), dim3(256), 0, st, part, nb, ld, ncols, seg,
                        o0, o1, o2, accumulate, scale);
   else
     hipLaunchKernelGGL(part_reduce_kernel<8>, dim3(ceil_div(ncols, 8)), dim3(256), 0, st, part, nb, ld, ncols, seg,
                        o0, o1, o2, accumulate, scale);
+  if (in_arena && !g_red.b.n) g_red.used = 0;
 }
 
 // ------------------------------------------------------------------ colsum
@@ -828,6 +909,33 @@ int fer::set_step_ptr_misc(const uint64_t* p) { return set_step_ptr_here(p) == h
 
 extern "C" int64_t fer_colsum_ws(int M, int N) { return (int64_t)colsum_nblk(M) * N * 4; }
 
+extern "C" int fer_reduce_defer(int mode, void* arena, int64_t arena_bytes, fer_stream_t stream) {
+  if (mode == 2) {  // pause: keep the queue, stop taking new reductions
+    g_red.take = false;
+    return 0;
+  }
+  if (mode != 0 && mode != 1) return set_error("reduce_defer: mode must be 0, 1 or 2");
+  const bool same = g_red.on && g_red.arena == (char*)arena && g_red.cap == (size_t)arena_bytes &&
+                    g_red.st == (hipStream_t)stream;
+  if (g_red.on && (mode == 0 || !same)) {
+    const int rc = red_flush();
+    g_red.on = g_red.take = false;
+    if (rc) return rc;
+  }
+  if (mode == 0) return 0;
+  if (!arena || arena_bytes < 65536) return set_error("reduce_defer: arena too small");
+  if (!same) {
+    g_red.arena = (char*)arena;
+    g_red.cap = (size_t)arena_bytes;
+    g_red.st = (hipStream_t)stream;
+    g_red.used = 0;
+  }
+  g_red.on = g_red.take = true;
+  return 0;
+}
+
+extern "C" int fer_reduce_flush(void) { return g_red.on ? red_flush() : 0; }
+
 extern "C" int fer_colsum(int dtype, const void* x, int64_t ldx, int M, int N, float* out, int accumulate,
                           const float* scale_ptr, float* ws, int64_t ws_bytes, fer_stream_t stream) {
   if (N <= 0) return 0;
@@ -836,6 +944,7 @@ extern "C" int fer_colsum(int dtype, const void* x, int64_t ldx, int M, int N, f
   if (!ws || ws_bytes < fer_colsum_ws(M, N)) return set_error("colsum: workspace too small");
   const int rpb = ceil_div(std::max(M, 1), nblk);
   hipStream_t st = (hipStream_t)stream;
+  ws = reduction_ws(ws, (size_t)fer_colsum_ws(M, N), N, st);
   dim3 grid(ceil_div(N / 4, 64), nblk);
   if (dtype == FER_BF16)
     hipLaunchKernelGGL(colsum_part_kernel<bf16>, grid, dim3(256), 0, st, (const bf16*)x, (long)ldx, M, N, ws, rpb);

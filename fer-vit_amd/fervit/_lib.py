@@ -67,6 +67,8 @@ SIGNATURES = {
                                 f32, u64, fp, i32, vp]),
     "fer_colsum_ws": (i64, [i32, i32]),
     "fer_colsum": (i32, [i32, vp, i64, i32, i32, fp, i32, fp, fp, i64, vp]),
+    "fer_reduce_defer": (i32, [i32, vp, i64, vp]),
+    "fer_reduce_flush": (i32, []),
     "fer_im2col_patch": (i32, [i32, fp, i32, i32, i32, i32, i32, vp, i64, vp]),
     "fer_tokens_fwd": (i32, [i32, vp, fp, fp, vp, i32, i32, i32, u32, f32, u64, vp]),
     "fer_tokens_bwd_ws": (i64, [i32, i32, i32]),

@@ -16,6 +16,7 @@ Layer math (reference):
 """
 from __future__ import annotations
 
+import functools
 from dataclasses import dataclass
 from typing import List, Optional, Sequence
 
@@ -24,6 +25,8 @@ import os
 import torch
 
 from . import ops
+from . import runtime
+from ._lib import check, lib
 from .runtime import WGRAD, FlatParams, grads_ready, next_seed
 
 
@@ -70,11 +73,80 @@ def _targets(flat: FlatParams, params: Sequence[torch.nn.Parameter], needs: Sequ
     return outs, bool(accs and accs[0])
 
 
+class _ReduceDefer:
+    """Deferred bias / LayerNorm gradient reductions over one backward pass (csrc/misc.hip
+    fer_reduce_defer). Inside a layer's backward the LayerNorm / attention / fused-GEMM column
+    partials go to a persistent arena and their fixed-order sums (`part_reduce`, ~4-5 per layer,
+    each a short dependent launch on the compute stream) are queued; the end of the backward (an
+    autograd-engine callback), a gradient-ready hook (DDP buckets) or a full queue runs them as ONE
+    launch. Bit-identical to the immediate reductions. Only the layer functions below open the
+    window (they write gradients into the flat buffer, which nothing reads before the backward
+    ends); every other caller of the same ops keeps the immediate path. FERVIT_REDUCE_DEFER=0 turns
+    it off (A/B); FERVIT_REDUCE_ARENA_MB sizes the arena (default 64 MB; a full arena flushes) and
+    csrc FERVIT_REDUCE_MAX_KB the largest partial set it takes (default 2 MB: small-token configs)."""
+
+    def __init__(self):
+        self.enabled = os.environ.get("FERVIT_REDUCE_DEFER", "1") != "0"
+        self.mb = int(os.environ.get("FERVIT_REDUCE_ARENA_MB", "64"))
+        self.arena: Optional[torch.Tensor] = None
+        self.open = False
+        self.windows = 0  # backward passes that deferred (tests)
+
+    def begin(self, device) -> bool:
+        if not self.enabled or device is None or device.type != "cuda":
+            return False
+        if not self.open:
+            if self.arena is None or self.arena.device != device:
+                if torch.cuda.is_current_stream_capturing():
+                    return False  # allocate in an eager step first (StepGraph warm-up)
+                self.arena = torch.empty(self.mb << 18, dtype=torch.float32, device=device)
+            try:
+                torch.autograd.Variable._execution_engine.queue_callback(self._end)
+            except RuntimeError:  # not inside a backward pass
+                return False
+            self.open = True
+            self.windows += 1
+        check(lib().fer_reduce_defer(1, self.arena.data_ptr(), self.arena.numel() * 4, ops.stream()), "reduce_defer")
+        return True
+
+    def pause(self) -> None:
+        check(lib().fer_reduce_defer(2, None, 0, None), "reduce_defer")
+
+    def flush(self) -> None:
+        if self.open:
+            check(lib().fer_reduce_flush(), "reduce_flush")
+
+    def _end(self) -> None:
+        self.open = False
+        check(lib().fer_reduce_defer(0, None, 0, None), "reduce_defer")
+
+
+REDUCE = _ReduceDefer()
+
+
+def _deferred_reductions(backward):
+    """Layer backward inside a deferred-reduction window (see _ReduceDefer)."""
+
+    @functools.wraps(backward)
+    def wrapped(ctx, *grads):
+        flat = getattr(ctx, "flat", None)
+        on = REDUCE.begin(getattr(flat, "device", None))
+        try:
+            return backward(ctx, *grads)
+        finally:
+            if on:
+                REDUCE.pause()
+
+    return wrapped
+
+
 def _finish(flat: FlatParams, params, needs) -> None:
     done = [p for p, n in zip(params, needs) if n]
     for p in done:
         flat.attach(p)
     if done:
+        if runtime._HOOKS:  # a hook (DDP bucket all-reduce) reads them: queued sums first
+            REDUCE.flush()
         grads_ready(done)
 
 
@@ -161,6 +233,7 @@ class PostNormLayerFn(torch.autograd.Function):
         return out
 
     @staticmethod
+    @_deferred_reductions
     def backward(ctx, dout):
         cfg, flat, P, seeds = ctx.cfg, ctx.flat, ctx.P, ctx.seeds
         in_w, in_b, out_w, out_b, w1, b1, w2, b2, n1w, n1b, n2w, n2b = P
@@ -248,6 +321,7 @@ class PreNormBlockFn(torch.autograd.Function):
         return out
 
     @staticmethod
+    @_deferred_reductions
     def backward(ctx, dout):
         cfg, flat, P = ctx.cfg, ctx.flat, ctx.P
         n1w, n1b, qkv_w, qkv_b, proj_w, proj_b, n2w, n2b, fc1_w, fc1_b, fc2_w, fc2_b = P
@@ -301,6 +375,7 @@ class AdapterFn(torch.autograd.Function):
         return out
 
     @staticmethod
+    @_deferred_reductions
     def backward(ctx, dout):
         flat, P = ctx.flat, ctx.P
         fc1_w, fc1_b, fc2_w, fc2_b, alpha = P
@@ -349,6 +424,7 @@ class PatchTokensFn(torch.autograd.Function):
         return t
 
     @staticmethod
+    @_deferred_reductions
     def backward(ctx, dt_):
         cfg, flat, P = ctx.cfg, ctx.flat, ctx.P
         proj_w, proj_b, cls, pos = P
@@ -385,6 +461,7 @@ class LatentTokensFn(torch.autograd.Function):
         return t
 
     @staticmethod
+    @_deferred_reductions
     def backward(ctx, dt_):
         cfg, flat, P = ctx.cfg, ctx.flat, ctx.P
         in_w, in_b, cls, pos = P
@@ -424,6 +501,7 @@ class HeadFn(torch.autograd.Function):
         return logits
 
     @staticmethod
+    @_deferred_reductions
     def backward(ctx, dlogits):
         cfg, flat, P = ctx.cfg, ctx.flat, ctx.P
         lnw, lnb, W, b = P
@@ -460,6 +538,7 @@ class WplusFn(torch.autograd.Function):
         return y
 
     @staticmethod
+    @_deferred_reductions
     def backward(ctx, dy):
         from ._lib import check, lib
 

@@ -158,6 +158,17 @@ int64_t fer_colsum_ws(int M, int N);
 int fer_colsum(int dtype, const void* x, int64_t ldx, int M, int N, float* out, int accumulate,
                const float* scale_ptr, float* ws, int64_t ws_bytes, fer_stream_t stream);
 
+/* Deferred gradient reductions (the framework's backward pass; no reference counterpart: the
+ * reference's bias / LayerNorm gradients come out of torch autograd one kernel each). mode 1
+ * opens (or resumes) a window: fer_layernorm_bwd / fer_attention_bwd / fer_colsum / fused GEMM
+ * column sums issued on `stream` write their per-block column partials into `arena` and queue the
+ * fixed-order partial sum instead of launching it; mode 2 pauses (the queue stays, new calls run
+ * immediately); mode 0 flushes and closes. fer_reduce_flush runs every queued sum as ONE launch on
+ * that stream (bit-identical to the immediate path). Callers flush before anything reads those
+ * gradients. Host state is per process (one window at a time). */
+int fer_reduce_defer(int mode, void* arena, int64_t arena_bytes, fer_stream_t stream);
+int fer_reduce_flush(void);
+
 /* Patch im2col (nn.Conv2d k=P,s=P, `image_vit.py:27-43`): x fp32 NCHW [B][C][Hh][Ww] ->
  * cols [B*gh*gw][ldc] in (c,kh,kw) order, cast to dtype. */
 int fer_im2col_patch(int dtype, const float* x, int B, int C, int Hh, int Ww, int P, void* cols, int64_t ldc,
