@@ -69,12 +69,45 @@ struct RedBatch {
   RedDesc d[kRedMax];
   int n;
 };
+// The batch kernel: 64 columns per block (a wave reads 256 contiguous bytes of a partial row,
+// where part_reduce_kernel<8>'s 8-column blocks read 32-byte pieces -- it needs narrow blocks to
+// spread one small reduction over the CUs; a batch has blocks enough). Lane = column, wave w owns
+// the row phases j = 8w .. 8w+7 of part_reduce_kernel<8> (RP = 32) and runs each with the same
+// eight accumulators in the same order, then the phases are summed in order j = 0..31: the same
+// float operations per column as the immediate kernel, so bit-identical.
 __global__ __launch_bounds__(256) void part_reduce_multi_kernel(const RedBatch b) {
+  constexpr int RP = 32;
+  __shared__ float red[RP][65];
   int i = 0;
   while (i + 1 < b.n && (int)blockIdx.x >= b.d[i + 1].blk0) ++i;
   const RedDesc& d = b.d[i];
-  part_reduce_body<8>(d.part, d.nb, d.ld, d.ncols, d.seg, d.o[0], d.o[1], d.o[2], d.accumulate, nullptr,
-                      blockIdx.x - d.blk0);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = (blockIdx.x - d.blk0) * 64 + lane;
+  const float* __restrict__ part = d.part;
+  const int nb = d.nb;
+  const long ld = d.ld;
+  for (int jj = 0; jj < 8; ++jj) {
+    const int j = w * 8 + jj;
+    float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (c < d.ncols) {
+      int bb = j;
+      for (; bb + 7 * RP < nb; bb += 8 * RP) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s[u] += part[(long)(bb + RP * u) * ld + c];
+      }
+      for (int u = 0; bb < nb; bb += RP, ++u) s[u] += part[(long)bb * ld + c];
+    }
+    red[j][lane] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+  }
+  __syncthreads();
+  if (w == 0 && c < d.ncols) {
+    float t = 0.f;
+#pragma unroll 8
+    for (int k = 0; k < RP; ++k) t += red[k][lane];
+    const int k = c / d.seg, col = c - k * d.seg;
+    float* o = k == 0 ? d.o[0] : (k == 1 ? d.o[1] : d.o[2]);
+    if (o) o[col] = d.accumulate ? o[col] + t : t;
+  }
 }
 static struct {
   bool on = false, take = false;  // window open (queue valid) / taking new reductions
@@ -119,7 +152,7 @@ void part_reduce(const float* part, int nb, long ld, int ncols, int seg, float* 
       for (float* o : {o0, o1, o2}) dup |= o && g_red.b.d[i].o[k] == o;
   if (in_arena && !scale && red_batchable(ncols) && g_red.b.n < kRedMax && !dup) {
     g_red.b.d[g_red.b.n++] = RedDesc{part, ld, {o0, o1, o2}, nb, ncols, seg, accumulate, g_red.blocks};
-    g_red.blocks += ceil_div(ncols, 8);
+    g_red.blocks += ceil_div(ncols, 64);
     return;
   }
   if (g_red.b.n && (in_arena || dup)) {  // run the queue first; this call's partials stay valid
