@@ -84,3 +84,64 @@ def test_deferred_reductions_grad_accumulation():
             REDUCE.enabled = True
     for k in out[0]:
         assert torch.equal(out[0][k], out[1][k]), k
+
+
+def test_reduce_defer_c_api_contract():
+    """fer_reduce_defer / fer_reduce_flush driven directly: a queued sum leaves its outputs untouched
+    until the flush; a second update of a queued output runs the queue first (stream order, so an
+    accumulate lands on the finished value); a paused window and a partial set above the arena run
+    immediately; closing the window flushes."""
+    from fervit import ops
+    from fervit._lib import check, lib
+
+    M, D = 4864, 512  # LayerNorm partials 304 x 3D fp32 = 1.9 MB: a deferrable set
+    g = torch.Generator(device="cuda").manual_seed(3)
+    x = torch.randn(M, D, device="cuda", generator=g).to(torch.bfloat16)
+    dy = torch.randn(M, D, device="cuda", generator=g).to(torch.bfloat16)
+    w = torch.rand(D, device="cuda", generator=g) + 0.5
+    b = torch.zeros(D, device="cuda")
+    mean = torch.empty(M, device="cuda")
+    rstd = torch.empty(M, device="cuda")
+    ops.layernorm_fwd(x, w, b, 1e-5, mean=mean, rstd=rstd)
+
+    def run(dg, db, acc=False):
+        ops.layernorm_bwd(dy, x, mean, rstd, w, dgamma=dg, dbeta=db, accumulate=acc)
+
+    g_ref, b_ref = torch.empty(D, device="cuda"), torch.empty(D, device="cuda")
+    run(g_ref, b_ref)
+    arena = torch.empty(16 << 18, device="cuda")  # 16 MB
+    st = ops.stream()
+    dg, db = torch.full((D,), 7.0, device="cuda"), torch.full((D,), 7.0, device="cuda")
+    check(lib().fer_reduce_defer(1, arena.data_ptr(), arena.numel() * 4, st), "defer")
+    try:
+        run(dg, db)
+        torch.cuda.synchronize()
+        assert (dg == 7.0).all() and (db == 7.0).all()  # queued
+        run(dg, db, acc=True)  # same outputs: the queue runs first, then this one
+        torch.cuda.synchronize()
+        assert torch.equal(dg, g_ref + g_ref) and torch.equal(db, b_ref + b_ref)
+        check(lib().fer_reduce_defer(2, None, 0, None), "pause")
+        dg2, db2 = torch.full((D,), 7.0, device="cuda"), torch.full((D,), 7.0, device="cuda")
+        run(dg2, db2)  # paused: immediate
+        torch.cuda.synchronize()
+        assert torch.equal(dg2, g_ref) and torch.equal(db2, b_ref)
+        check(lib().fer_reduce_defer(1, arena.data_ptr(), arena.numel() * 4, st), "resume")
+        dg3, db3 = torch.full((D,), 7.0, device="cuda"), torch.full((D,), 7.0, device="cuda")
+        run(dg3, db3)
+        check(lib().fer_reduce_flush(), "flush")
+        torch.cuda.synchronize()
+        assert torch.equal(dg3, g_ref) and torch.equal(db3, b_ref)
+        run(dg3, db3, acc=True)  # queued again; closing the window flushes it
+    finally:
+        check(lib().fer_reduce_defer(0, None, 0, None), "close")
+    torch.cuda.synchronize()
+    assert torch.equal(dg3, g_ref + g_ref)
+    small = torch.empty(65536 // 4, device="cuda")  # a 64 KB arena: the 1.9 MB set cannot be taken
+    dg4, db4 = torch.full((D,), 7.0, device="cuda"), torch.full((D,), 7.0, device="cuda")
+    check(lib().fer_reduce_defer(1, small.data_ptr(), small.numel() * 4, st), "defer")
+    try:
+        run(dg4, db4)
+        torch.cuda.synchronize()
+        assert torch.equal(dg4, g_ref) and torch.equal(db4, b_ref)
+    finally:
+        check(lib().fer_reduce_defer(0, None, 0, None), "close")
