@@ -132,10 +132,10 @@ def gemm_algo_bytes(d, e) -> int:
 class GemmProbe:
     """HIP events around every gemm_8ph launch, on the launch stream (probe phase only)."""
 
-    def __init__(self):
+    def __init__(self, probe_all=False):
         self.rec = []
-        self.other = []  # FERVIT_PROBE_ALL=1: every other GEMM launch too (stderr table, not the JSON line)
-        self.all = os.environ.get("FERVIT_PROBE_ALL") == "1"
+        self.other = []  # --probe-all: every other GEMM launch too (stderr table, not the JSON line)
+        self.all = probe_all
         self.on = False
 
     def __call__(self, d, e, launch):
@@ -236,6 +236,20 @@ def pmc_traffic(timeout_s=240):
                                         "2*FETCH_SIZE (gfx950 16 B/lane correction)"}
 
 
+def cpu_model() -> str:
+    """Host CPU model name (/proc/cpuinfo, as `lscpu` reports it)."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+
+    return platform.processor() or "unknown"
+
+
 def cpu_baseline(cfg_name, budget_s=12.0, bs=None):
     """Oracle train step (fp32, torch CPU ops: oracle/vit_oracle.py, zero_grad -> fwd (dropout
     0.1) -> CE(ls 0.1) -> bwd -> AdamW as `train/train_image_vit.py:117-130`) on a bounded
@@ -302,7 +316,7 @@ def cpu_baseline(cfg_name, budget_s=12.0, bs=None):
             break
     times.sort()
     med = times[len(times) // 2]
-    return {"value": round(bs / med, 3), "unit": "images/s", "cores": threads, "kind": "port",
+    return {"value": round(bs / med, 3), "unit": "images/s", "cores": threads, "cpu_model": cpu_model(), "kind": "port",
             "sample": f"{cfg_name}: oracle train step (fwd+bwd+AdamW, fp32, dropout 0.1, CE ls 0.1) at bs={bs}, "
                       f"{len(times)} timed steps, median {med * 1e3:.0f} ms/step, torch {torch.__version__}"}
 
@@ -342,6 +356,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC traffic passes")
     ap.add_argument("--probe-steps", type=int, default=2, help="steps of the (untimed) roofline probe phase")
+    ap.add_argument("--probe-all", action="store_true",
+                    help="probe phase: time every other GEMM launch too (stderr table, not the JSON line)")
     ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
                     help="replay the whole step as a HIP graph (auto: on for the launch-bound small configs)")
     ap.add_argument("--grad-dtype", choices=["fp32", "bf16"], default="fp32",
@@ -376,9 +392,6 @@ def main():
         traffic, traffic_detail = pmc_traffic()
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
-    prio = os.environ.get("FERVIT_STEP_PRIO")
-    if prio is not None:  # A/B: run the step on a stream of this priority (the weight-gradient stream keeps 0)
-        torch.cuda.set_stream(torch.cuda.Stream(device=device, priority=int(prio)))
     rccl = None
     if world > 1:
         dist.init_process_group("nccl", device_id=device)
@@ -417,7 +430,7 @@ def main():
         trunk = gemm_flops_per_img(D, L, F, N) // 3
         adapters = L * 2 * N * (2 * D * 64)
         flops_img = 2 * trunk + 3 * (adapters + 2 * 18 * 512 * D + 2 * D * 7)
-    probe = GemmProbe()
+    probe = GemmProbe(args.probe_all)
     ops.LAUNCH_PROBE = probe
 
     def step():
@@ -456,15 +469,20 @@ def main():
         el = t.item()
     step_ms = [ev[i].elapsed_time(ev[i + 1]) for i in range(args.steps)]
     lossv = loss.item()
-    # probe phase (untimed): HIP events around every gemm_8ph launch of a few eager steps
+    # probe phases (untimed): HIP events around every gemm_8ph launch of a few eager steps.
+    # In-step: as the timed steps run them (weight-gradient stream on, so a launch may share the chip
+    # with a concurrent split-K weight gradient); isolated (the roofline `frac`): weight-gradient
+    # stream off, every launch alone on the chip.
     if use_graph:
         graph.release()
-    # the weight-gradient stream is switched off for the probe: with it, a dgrad launch shares the
-    # chip with a concurrent split-K wgrad and its events would time that contention (and the wait
-    # for CUs the wgrad holds), not the kernel
+    probe.on = True
+    for _ in range(args.probe_steps):
+        step()
+    torch.cuda.synchronize()
+    ps_in = probe.summary(args.probe_steps)
+    probe.rec, probe.other = [], []
     wg_on = runtime.WGRAD.enabled
     runtime.WGRAD.enabled = False
-    probe.on = True
     for _ in range(args.probe_steps):
         step()
     torch.cuda.synchronize()
@@ -477,6 +495,7 @@ def main():
     imgs = world * B * args.steps / el
     step_tflops = flops_img * B / (ms / 1e3) / 1e12
     achieved = ps["flop_per_launch"] / (ps["mean_launch_ms"] / 1e3) / 1e12 if ps["launches"] else 0.0
+    achieved_in = ps_in["flop_per_launch"] / (ps_in["mean_launch_ms"] / 1e3) / 1e12 if ps_in["launches"] else 0.0
     if rank == 0:
         cpu = cpu1 = None
         if world == 1 and not args.no_cpu_baseline:
@@ -495,6 +514,11 @@ def main():
                                                     "patch embed, fused epilogues)",
                          "achieved": round(achieved, 1), "peak": round(PEAK_BF16_TFLOPS, 1), "unit": "TFLOP/s",
                          "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
+                         "frac_in_step": round(achieved_in / PEAK_BF16_TFLOPS, 4),
+                         "mean_launch_ms_in_step": round(ps_in["mean_launch_ms"], 4),
+                         "frac_note": "frac: each launch alone on the chip (weight-gradient stream off); "
+                                      "frac_in_step: the same launches in eager train steps with the "
+                                      "weight-gradient stream on (sharing CUs with split-K weight gradients)",
                          "traffic": None if traffic is None else round(traffic),
                          "traffic_detail": traffic_detail,
                          "algorithmic_bytes": round(ps["algo_bytes_per_launch"]),

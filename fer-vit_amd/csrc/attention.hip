@@ -270,50 +270,12 @@ FER_DEV void fwd_load_q(bf16x8 (&qf)[4], const bf16* qkv, long ldq, int unit, in
   }
 }
 
-// Keep-bit words of the persistent path, computed ahead of the forward (data-independent: only the
-// seed and the element indices enter). Layout as attn_fwd_pers documents: word ((bh*NB + kb)*NB +
-// qb)*32 + j = bits over the 32 queries of block qb for key kb*32 + j, the same hash of the same
-// element index for every (query, key) -- padding rows / keys included -- so the words are the ones
-// the forward's ballots produced. Thread = (bh, kb, qb, key pair jp): 32 hashes, two words (keys
-// 2jp, 2jp+1 = the two 16-bit halves of one hash), one 8-byte store (16 threads = one 128-byte row).
-// (Opt-in, FERVIT_ATTN_MASK_PRE=1: measured no faster than hashing inside the forward.)
-__global__ __launch_bounds__(256) void attn_mask_gen(uint32_t* __restrict__ mask, int BH, int N, int NB, uint32_t thr,
-                                                     uint64_t seed) {
-  seed = step_seed(seed);
-  const long t = (long)blockIdx.x * 256 + threadIdx.x;
-  const long blk = t >> 4;  // (bh, kb, qb)
-  if (blk >= (long)BH * NB * NB) return;
-  const int jp = (int)(t & 15);
-  const int qb = (int)(blk % NB), kb = (int)((blk / NB) % NB), bh = (int)(blk / ((long)NB * NB));
-  const uint32_t kpair = (uint32_t)(kb * 16 + jp);  // (kb*32 + 2*jp) >> 1
-  const uint32_t thr_hi = thr << 16;
-  uint32_t w0 = 0, w1 = 0;
-#pragma unroll 8
-  for (int i = 0; i < 32; ++i) {
-    const uint32_t h = fer_hash(seed, (drop_row(bh, N, qb * 32 + i) >> 1) + kpair);
-    w0 |= (uint32_t)((h & 0xFFFFu) >= thr) << i;
-    w1 |= (uint32_t)(h >= thr_hi) << i;
-  }
-  *(uint2*)(mask + blk * 32 + 2 * jp) = uint2{w0, w1};
-}
-
-// Dropout of the 16 S^T accumulator registers from precomputed keep words (attn_mask_gen): the
-// 64-bit lane mask of register r is (word of key a) | (word of key a+4) << 32 with a = acc_row(r, 0)
-// -- lane l holds query l & 31 and, in the upper half, key a + 4 -- i.e. exactly the ballot the
-// forward used to take of its keep compares (inverse ballot: one v_cndmask per element with the
-// SGPR pair as its lane mask), the words by scalar loads.
-FER_DEV float keep_sel(float v, uint64_t lanemask) {
-  return __builtin_amdgcn_inverse_ballot_w64(lanemask) ? v : 0.f;
-}
-
-template <int NB, bool PRE = false>
+template <int NB>
 __global__ __launch_bounds__(64 * (NB + 1)) void attn_fwd_pers(const bf16* __restrict__ qkv, long ldq,
                                                                bf16* __restrict__ out, long ldo,
                                                                float* __restrict__ lse, uint32_t* __restrict__ mask,
                                                                int BH, int N, int H, int dh, float sl2, uint32_t thr,
                                                                float dscale, uint64_t seed, WqArgs wq) {
-  // PRE: the keep words were written by attn_mask_gen; this kernel reads them (scalar loads) instead
-  // of hashing, ballotting and storing them
   seed = step_seed(seed);
   constexpr int IMG = NB * 32 * 128;
   __shared__ __attribute__((aligned(1024))) char lds[4 * IMG + 16];  // 2 x (K image, V image), unit hand-off
@@ -371,13 +333,6 @@ __global__ __launch_bounds__(64 * (NB + 1)) void attn_fwd_pers(const bf16* __res
       for (int s = 0; s < 4; ++s) kfr[s] = rd_row(Ki, lane & 31, 2 * s + hh);
       // softmax + dropout + P.V of key block kb, whose S^T is in st
       auto block = [&](int kb, f32x16& st) {
-        uint32_t kw[32];  // PRE: this block's keep words, loaded (scalar) ahead of the softmax
-        if (PRE) {
-          const __attribute__((address_space(4))) uint32_t* mw =
-              (const __attribute__((address_space(4))) uint32_t*)(mask + (((long)bh * NB + kb) * NB + w) * 32);
-#pragma unroll
-          for (int j = 0; j < 32; ++j) kw[j] = mw[j];
-        }
         bf16x8 vfr[2][2];
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2)
@@ -406,13 +361,7 @@ __global__ __launch_bounds__(64 * (NB + 1)) void attn_fwd_pers(const bf16* __res
           st[r] = ex2(fmaf(st[r], sl2, -m));
           l += st[r];
         }
-        if (PRE) {
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int a = acc_row(r, 0);
-            st[r] = keep_sel(st[r], (uint64_t)kw[a] | ((uint64_t)kw[a + 4] << 32));
-          }
-        } else if (thr) {
+        if (thr) {
           const uint32_t p0 = (row >> 1) + kb * 16 + 2 * hh;  // hash pair of register 0
           uint64_t bal[16];
 #pragma unroll
@@ -554,8 +503,7 @@ __global__ __launch_bounds__(64 * NB) void attn_bwd_fused_bf16(const bf16* __res
                                                                const float* __restrict__ lse,
                                                                bf16* __restrict__ dqkv, long lddq, int N, int H,
                                                                int dh, float scale, float sl2, uint32_t thr,
-                                                               float dscale, uint64_t seed, float* __restrict__ cs_part,
-                                                               int dbg) {
+                                                               float dscale, uint64_t seed, float* __restrict__ cs_part) {
   seed = step_seed(seed);
   constexpr int IMG = NB * 32 * 128;
   __shared__ __attribute__((aligned(1024))) char lds[fused_lds_bytes<NB>()];
@@ -574,7 +522,7 @@ __global__ __launch_bounds__(64 * NB) void attn_bwd_fused_bf16(const bf16* __res
   for (int t = threadIdx.x; t < NB * 64; t += 64 * NB) {
     const int qr = t >> 1, half = t & 1;
     float dsum = 0.f;
-    if (qr < N && !(dbg & 1)) {
+    if (qr < N) {
       const bf16* po = out + ((long)b * N + qr) * ldo + h * dh;
       const bf16* pd = dout + ((long)b * N + qr) * lddo + h * dh;
       for (int d = half * 8; d < dh; d += 16) {
@@ -608,7 +556,7 @@ __global__ __launch_bounds__(64 * NB) void attn_bwd_fused_bf16(const bf16* __res
   const bool odd = lane & 1;
   f32x16 dk[2] = {f32x16{}, f32x16{}}, dv[2] = {f32x16{}, f32x16{}};
   f32x16 dq[2] = {f32x16{}, f32x16{}};  // dQ^T of query block w (this wave owns it), registers
-  const int nsteps = (dbg & 2) ? 0 : NB;
+  const int nsteps = NB;
 #pragma unroll 1
   for (int i = 0; i < nsteps; ++i) {
     int qb = w + i;
@@ -796,9 +744,7 @@ template <int NB>
 __global__ __launch_bounds__(64 * NB) void attn_bwd_pers(
     const bf16* __restrict__ qkv, long ldq, const bf16* __restrict__ out, long ldo, const bf16* __restrict__ dout,
     long lddo, const float* __restrict__ lse, const uint32_t* __restrict__ mask, bf16* __restrict__ dqkv, long lddq,
-    int BH, int N, int H, int dh, float scale, float sl2, float dscale, float* __restrict__ cs_part, int dbg,
-    WqArgs wq) {
-  // dbg (FERVIT_ATTN_DBG, timing experiments only): 1 = no step math, 2 = no epilogue stores
+    int BH, int N, int H, int dh, float scale, float sl2, float dscale, float* __restrict__ cs_part, WqArgs wq) {
   constexpr int IMG = NB * 32 * 128;
   constexpr int PREP = NB >= 4 ? 3 : NB - 1;  // step whose dQ phase computes the next unit's Dq
   __shared__ __attribute__((aligned(1024))) char lds[pers_bwd_lds_bytes<NB>() + 16];
@@ -906,7 +852,7 @@ __global__ __launch_bounds__(64 * NB) void attn_bwd_pers(
     // register it touches into a loop-carried copy
     auto step = [&](int i, auto last_tag) {
       constexpr bool LAST = decltype(last_tag)::value;
-      if (!(dbg & 1)) {
+      {
         int lane = threadIdx.x & 63;  // laundered per step: lane-derived LDS addresses are not
         asm volatile("" : "+v"(lane));  // hoisted out of the step loop (they would pin ~40 VGPRs)
         const int hh = lane >> 5;
@@ -974,7 +920,7 @@ __global__ __launch_bounds__(64 * NB) void attn_bwd_pers(
         }
       }
       bar_lds();  // every dS tile of this step is in Sall
-      if (!(dbg & 1)) {
+      {
         int lane = threadIdx.x & 63;
         asm volatile("" : "+v"(lane));
         const int hh = lane >> 5;
@@ -1027,12 +973,11 @@ __global__ __launch_bounds__(64 * NB) void attn_bwd_pers(
     step(NB - 1, std::true_type{});
     // ---- epilogue of unit u (one barrier)
     if (has_next) {
-      if (PREP == NB - 1 && (dbg & 1)) prep_finish(un, cur ^ 1);
       // the claim's round trip overlaps this wait for the next unit's rows
       if (wq.q && threadIdx.x == 0) unn = wq_claim(wq.q, wq.base, BH);
       wait_vm<0>();  // this wave's DMA rows of the next unit, its K / V fragments, its mask word
     }
-    if (!(dbg & 2)) {
+    {
       const int b = u / H, h = u - b * H;
       const int q = w * 32 + (lane & 31);
       if (q < N) {  // dQ^T: lane = query, registers = 4 consecutive d per group
@@ -1585,8 +1530,7 @@ extern "C" int fer_attention_fwd(int dtype, const void* qkv, int64_t ld_qkv, voi
   if (ld_qkv % 8 || ld_out % 4) return set_error("attention_fwd(bf16): misaligned leading dimension");
   if ((long)B * N * ld_qkv * 2 >= 0x7FFFFFF0L) return set_error("attention_fwd(bf16): qkv exceeds 2 GiB");
   const float sl2 = scale * LOG2E;
-  static const bool old_fwd = getenv("FERVIT_ATTN_FWD_OLD") != nullptr;  // A/B switch (no mask: p = 0 only)
-  if (N <= 256 && dh <= 64 && ((old_fwd && !drop_thresh) || N > 224)) {  // NB = 8: 9 waves would not fit 2/SIMD
+  if (N <= 256 && dh <= 64 && N > 224) {  // NB = 8: 9 waves would not fit 2/SIMD
     const int nb = (N + 31) / 32;
     FER_NB_SWITCH(nb, hipLaunchKernelGGL(attn_fwd_bf16<NB_>, dim3(B * H), dim3(64 * NB_), 0, st, (const bf16*)qkv,
                                          (long)ld_qkv, (bf16*)out, (long)ld_out, lse, N, H, dh, sl2, drop_thresh,
@@ -1604,27 +1548,11 @@ extern "C" int fer_attention_fwd(int dtype, const void* qkv, int64_t ld_qkv, voi
 #undef FER_FOCC
     const int grid = std::min(B * H, n_cus() * occ);
     const WqArgs wq = fixed_stride() ? WqArgs{} : wq_prepare_here(st, grid, B * H);
-    // FERVIT_ATTN_MASK_PRE=1: keep words by attn_mask_gen ahead of the forward, which then selects
-    // with them instead of hashing (opt-in: the hashing costs the same VALU time in either kernel --
-    // ViT-B forward 135-138 us inline vs 153-155 us mask kernel + forward, step +0.1-0.3 ms,
-    // profiles/r03ad_attn_mask_pre_ab.txt)
-    static const bool pre_mask = getenv("FERVIT_ATTN_MASK_PRE") != nullptr;
-    const bool pre = mask && pre_mask;
-    if (pre) {
-      const long words = (long)B * H * nb * nb * 32;
-      hipLaunchKernelGGL(attn_mask_gen, dim3((unsigned)ceil_div(words / 2, 256)), dim3(256), 0, st, mask, B * H, N,
-                         nb, drop_thresh, seed);
-    }
-#define FER_FPERS(NBV)                                                                                       \
-  case NBV:                                                                                                  \
-    if (pre)                                                                                                 \
-      hipLaunchKernelGGL((attn_fwd_pers<NBV, true>), dim3(grid), dim3(64 * (NBV + 1)), 0, st, (const bf16*)qkv, \
-                         (long)ld_qkv, (bf16*)out, (long)ld_out, lse, mask, B * H, N, H, dh, sl2, drop_thresh, \
-                         drop_scale, seed, wq);                                                             \
-    else                                                                                                     \
-      hipLaunchKernelGGL((attn_fwd_pers<NBV, false>), dim3(grid), dim3(64 * (NBV + 1)), 0, st, (const bf16*)qkv, \
-                         (long)ld_qkv, (bf16*)out, (long)ld_out, lse, mask, B * H, N, H, dh, sl2, drop_thresh, \
-                         drop_scale, seed, wq);                                                             \
+#define FER_FPERS(NBV)                                                                                     \
+  case NBV:                                                                                                \
+    hipLaunchKernelGGL((attn_fwd_pers<NBV>), dim3(grid), dim3(64 * (NBV + 1)), 0, st, (const bf16*)qkv,    \
+                       (long)ld_qkv, (bf16*)out, (long)ld_out, lse, mask, B * H, N, H, dh, sl2, drop_thresh, \
+                       drop_scale, seed, wq);                                                             \
     break;
     switch (nb) {
       FER_FPERS(1) FER_FPERS(2) FER_FPERS(3) FER_FPERS(4) FER_FPERS(5) FER_FPERS(6) FER_FPERS(7)
@@ -1685,10 +1613,7 @@ extern "C" int fer_attention_bwd(int dtype, const void* qkv, int64_t ld_qkv, con
     return set_error("attention_bwd(bf16): operand exceeds 2 GiB (buffer-resource range)");
   const int nb = (N + 31) / 32;
   const float sl2 = scale * LOG2E;
-  static const bool general = getenv("FERVIT_ATTN_GENERAL") != nullptr;  // A/B switch: general path only
-  static const int dbg = getenv("FERVIT_ATTN_DBG") ? atoi(getenv("FERVIT_ATTN_DBG")) : 0;  // timing experiments
-  static const bool old_bwd = getenv("FERVIT_ATTN_BWD_OLD") != nullptr;  // A/B switch (p = 0 only)
-  if (pers_path(dtype, N, dh) && !general && !(old_bwd && !drop_thresh)) {
+  if (pers_path(dtype, N, dh)) {
     const uint32_t* mask = drop_thresh ? (const uint32_t*)(lse + lse_floats(B, N, H)) : nullptr;
     if (colsum) ws = reduction_ws(ws, (size_t)B * nb * D3 * 4, D3, st);
     int occ = 1;
@@ -1706,7 +1631,7 @@ extern "C" int fer_attention_bwd(int dtype, const void* qkv, int64_t ld_qkv, con
     hipLaunchKernelGGL(attn_bwd_pers<NBV>, dim3(grid), dim3(64 * NBV), 0, st, (const bf16*)qkv,                \
                        (long)ld_qkv, (const bf16*)out, (long)ld_out, (const bf16*)dout, (long)ld_dout, lse, mask, \
                        (bf16*)dqkv, (long)ld_dqkv, B * H, N, H, dh, scale, sl2, drop_scale, colsum ? ws : nullptr, \
-                       dbg, wq);                                                                                 \
+                       wq);                                                                                      \
     break;
     switch (nb) {
       FER_PERS(1) FER_PERS(2) FER_PERS(3) FER_PERS(4) FER_PERS(5) FER_PERS(6) FER_PERS(7)
@@ -1718,14 +1643,14 @@ extern "C" int fer_attention_bwd(int dtype, const void* qkv, int64_t ld_qkv, con
     part_reduce(ws, B * nb, D3, D3, D3, colsum, nullptr, nullptr, colsum_accumulate, nullptr, st);
     return hip_check("attention_bwd_colsum");
   }
-  if (nb <= 8 && dh <= 64 && !general) {
+  if (nb <= 8 && dh <= 64) {
     if (colsum) ws = reduction_ws(ws, (size_t)B * D3 * 4, D3, st);
 #define FER_FUSED(NBV)                                                                                       \
   case NBV:                                                                                                  \
     hipLaunchKernelGGL(attn_bwd_fused_bf16<NBV>, dim3(B * H), dim3(64 * NBV), 0, st, (const bf16*)qkv,       \
                        (long)ld_qkv, (const bf16*)out, (long)ld_out, (const bf16*)dout, (long)ld_dout, lse,   \
                        (bf16*)dqkv, (long)ld_dqkv, N, H, dh, scale, sl2, drop_thresh, drop_scale, seed,      \
-                       colsum ? ws : nullptr, dbg);                                                         \
+                       colsum ? ws : nullptr);                                                              \
     break;
     switch (nb) {  // every N <= 256
       FER_FUSED(1) FER_FUSED(2) FER_FUSED(3) FER_FUSED(4) FER_FUSED(5) FER_FUSED(6) FER_FUSED(7)

@@ -24,12 +24,9 @@ int hip_check(const char* what) {
   return 0;
 }
 
-static int g_fixed_stride = -1;  // -1: FERVIT_FIXED_STRIDE decides on first use
+static int g_fixed_stride = 0;  // fer_set_persistent_mode
 
-bool fixed_stride_mode() {
-  if (g_fixed_stride < 0) g_fixed_stride = getenv("FERVIT_FIXED_STRIDE") != nullptr ? 1 : 0;
-  return g_fixed_stride == 1;
-}
+bool fixed_stride_mode() { return g_fixed_stride == 1; }
 
 }  // namespace fer
 

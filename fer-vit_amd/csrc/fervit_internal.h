@@ -20,8 +20,6 @@ struct GemmArgs {
   int splits, k_chunk, partial;
   float* ws;
   float* cs_part;  // fused column sums: per-tile partials [tiles_m][N] (or null)
-  int dbg;  // experiment switches (FERVIT_GEMM_DBG), 0 in production
-  unsigned* cnt;  // split-K with the in-launch reduction: per-tile tickets (zeroed per launch), else null
   int* tq;               // persistent 8-phase kernel: work-queue counters (common.h wq_*), null = fixed stride
   unsigned tq_base[8];   // their values at launch
 };
@@ -34,7 +32,7 @@ int set_step_ptr_layernorm(const uint64_t* p);
 int set_step_ptr_misc(const uint64_t* p);
 int hip_check(const char* what);
 // persistent GEMM / attention kernels: walk a fixed blockIdx stride instead of the work queue
-// (fer_set_persistent_mode(1), or FERVIT_FIXED_STRIDE in the environment)
+// (fer_set_persistent_mode(1))
 bool fixed_stride_mode();
 int gemm_launch(const GemmDesc& d, const EpiArgs& e, hipStream_t st);
 inline int ceil_div(long a, long b);

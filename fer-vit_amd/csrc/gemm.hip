@@ -232,12 +232,6 @@ FER_DEV void epi8_k(const EpiArgs& e, long oc, long op, uint32_t di, f32x4& v0, 
       v0[r] = k0 ? fmaxf(v0[r], 0.f) : 0.f;
       v1[r] = k1 ? fmaxf(v1[r], 0.f) : 0.f;
     }
-#ifdef FER_GEMM_EXP
-    if (e.colsum_accumulate & 0x100) {
-      const bf16x8 pg = pack8(g0, g1);
-      asm volatile("" ::"v"(pg));
-    } else
-#endif
     *(bf16x8*)((bf16*)e.pre + op) = pack8(g0, g1);
   }
   if constexpr (S == EPI_GATE) {
@@ -257,12 +251,6 @@ FER_DEV void epi8_k(const EpiArgs& e, long oc, long op, uint32_t di, f32x4& v0, 
         g1[r] = kp[4 + r] ? g1[r] : 0.f;
       }
     }
-#ifdef FER_GEMM_EXP
-    if (e.colsum_accumulate & 0x100) {
-      const bf16x8 pg = pack8(g0, g1);
-      asm volatile("" ::"v"(pg));
-    } else
-#endif
     *(bf16x8*)((bf16*)e.pre + op) = pack8(g0, g1);
   }
   if constexpr (S == EPI_RES) {
@@ -282,13 +270,6 @@ FER_DEV void epi8_k(const EpiArgs& e, long oc, long op, uint32_t di, f32x4& v0, 
     v0 *= lo4(x);
     v1 *= hi4(x);
   }
-#ifdef FER_GEMM_EXP
-  if (e.colsum_accumulate & 0x100) {  // experiments library only: no output store (values kept live)
-    const bf16x8 pv = pack8(v0, v1);
-    asm volatile("" ::"v"(pv));
-    return;
-  }
-#endif
   *(bf16x8*)((bf16*)e.c + oc) = pack8(v0, v1);
 }
 
@@ -302,10 +283,9 @@ static inline int epi_kind(const EpiArgs& e) {
     return act == FER_ACT_GELU ? EPI_GATE : (act == FER_ACT_RELU ? EPI_GATER : EPI_GEN);
   }
   if (e.pre || act) return EPI_GEN;
-  static const bool xdma = getenv("FERVIT_EPI_XDMA") != nullptr;  // A/B: row operand through LDS-DMA
-  if (e.aux) return (e.aux_act == FER_ACT_MUL && !e.res && !e.drop_thresh) ? (xdma ? EPI_MUL : EPI_MUL2) : EPI_GEN;
+  if (e.aux) return (e.aux_act == FER_ACT_MUL && !e.res && !e.drop_thresh) ? EPI_MUL2 : EPI_GEN;
   if (e.colsum) return EPI_GEN;
-  if (e.res) return xdma ? EPI_RES : EPI_RES2;
+  if (e.res) return EPI_RES2;
   return e.drop_thresh ? EPI_GEN : EPI_STORE;
 }
 
@@ -535,63 +515,6 @@ FER_DEV void tile_epilogue(const GemmArgs& g, const EpiArgs& e, AccT (&acc)[FN][
   constexpr int NQ = MT == 32 ? 4 : 1;
   const int lr = MT == 32 ? (lane & 31) : (lane & 15);
   const int lc = MT == 32 ? 4 * (lane >> 5) : 4 * (lane >> 4);
-  if constexpr (EK == EPI_GEN) {
-    if (g.partial && g.cnt) {
-      // split-K, reduced in this launch: the partial goes to slab ks ([split][M][N] fp32) by
-      // write-through (sc1) stores; after every wave drained them, thread 0 takes a ticket from the
-      // tile's counter (agent-scope atomic; counters zeroed by the host before the launch). The split
-      // drawing the last ticket sums the tile's slabs by sc1 loads in split order and applies the
-      // epilogue -- the arithmetic of splitk_reduce_kernel element for element (bit-identical), with
-      // no second launch and the slabs still warm. (MI355X_MICROARCH.md, Workgroup dispatch: sc1
-      // stores / counter / sc1 loads, one workgroup per CU.)
-      const __amdgpu_buffer_rsrc_t rs = make_rsrc(g.ws);
-      const long MN = (long)g.M * g.N;
-#pragma unroll
-      for (int i = 0; i < FN; ++i)
-#pragma unroll
-        for (int j = 0; j < FM; ++j)
-#pragma unroll
-          for (int q = 0; q < NQ; ++q) {
-            const long m = m0 + wm * TM + j * MT + lr, n = n0 + wn * TN + i * MT + 8 * q + lc;
-            if (m < g.M && n < g.N)
-              __builtin_amdgcn_raw_buffer_store_b128(
-                  __builtin_bit_cast(u32x4, f32x4{acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2],
-                                                  acc[i][j][4 * q + 3]}),
-                  rs, (uint32_t)((ks * MN + m * g.N + n) * 4), 0, 16 /* sc1 */);
-          }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's partial is out
-      __syncthreads();  // every wave's partial is out; every wave is past the main loop's LDS reads
-      volatile unsigned* flag = (volatile unsigned*)smem;
-      if (tid_ == 0) {  // acquire after the last ticket, as in gemm_wgrad_group_kernel
-        const unsigned tk = __hip_atomic_fetch_add(g.cnt + (m0 / BM) + (n0 / BN) * g.tiles_m, 1u, __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_AGENT);
-        if (tk == (unsigned)(g.splits - 1)) {
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        *flag = tk;
-      }
-      __syncthreads();
-      const bool last = *flag == (unsigned)(g.splits - 1);
-      __syncthreads();  // the flag word is read before any later use of the LDS (persistent kernels)
-      if (!last) return;
-      const uint64_t seed = e.drop_thresh ? step_seed(e.seed) : 0;
-      constexpr int G4 = BN / 4, NT = 64 * WM * WN;
-      const int rows = min(BM, g.M - m0), cols4 = min(BN, g.N - n0) / 4;
-#pragma unroll 1
-      for (int idx = tid_; idx < BM * G4; idx += NT) {
-        const int r = idx / G4, c = idx - r * G4;
-        if (r >= rows || c >= cols4) continue;
-        const long m = m0 + r, n = n0 + 4 * c;
-        const uint32_t o = (uint32_t)((m * g.N + n) * 4);
-        f32x4 v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 16));
-        for (int sp = 1; sp < g.splits; ++sp)
-          v += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, o + (uint32_t)(sp * MN * 4), 0, 16));
-        epi4<bf16>(e, m, n, v, seed);
-      }
-      return;
-    }
-  }
   if (g.partial) {  // split-K partial slab, fp32 [split][M][N] (reduced by splitk_reduce_kernel)
     float* ws = g.ws + (long)ks * g.M * g.N;
 #pragma unroll
@@ -887,7 +810,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g, 
   const int wm = wave % WM, wn = wave / WM;
 
   int tm, tn, ks = 0;
-  if (gridDim.y > 1 && !(g.dbg & 16)) split_tile_of(g.tiles_m, g.tiles_n, tm, tn, ks);  // dbg 16: A/B
+  if (gridDim.y > 1) split_tile_of(g.tiles_m, g.tiles_n, tm, tn, ks);
   else {
     tile_of(blockIdx.x, g.tiles_m, g.tiles_n, tm, tn);
     ks = blockIdx.y;
@@ -929,14 +852,14 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g, 
     const bool more = t + 1 < nk;
     const int k1 = kbeg + (t + 1) * BK;
     // the whole of stage t+1 goes out first: it has the full K-step to land
-    if (more && !(g.dbg & 1)) {
+    if (more) {
       pa.issue(ra, nxt, wave, g.lda, k1, kend, k1 == ktail);
       pb.issue(rb, nxt + A_BYTES, wave, g.ldb, k1, kend, k1 == ktail);
     }
 #pragma unroll
     for (int kk = 0; kk < SS; ++kk) {
       bf16x8 an[FM], bn[FN];
-      if (kk < SS - 1 && !(g.dbg & 8)) {
+      if (kk < SS - 1) {
 #pragma unroll
         for (int i = 0; i < FN; ++i) bn[i] = read_frag<MT, BN, BKC>(cur + A_BYTES, wn * TN + i * MT, kk + 1, lane);
 #pragma unroll
@@ -946,14 +869,14 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g, 
       for (int j = 0; j < FM; ++j)
 #pragma unroll
         for (int i = 0; i < FN; ++i) acc[i][j] = mfma<MT>(bfr[i], af[j], acc[i][j]);
-      if (kk < SS - 1 && !(g.dbg & 8)) {
+      if (kk < SS - 1) {
 #pragma unroll
         for (int i = 0; i < FN; ++i) bfr[i] = bn[i];
 #pragma unroll
         for (int j = 0; j < FM; ++j) af[j] = an[j];
       }
     }
-    if (more && !(g.dbg & 2)) {
+    if (more) {
       wait_vm<0>();
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
@@ -964,10 +887,6 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g, 
     }
   }
 
-  if (g.dbg & 4) {
-    if (acc[0][0][0] == 12345.f) g.ws[0] = 1.f;  // keep the MFMAs alive
-    return;
-  }
   tile_epilogue<BM, BN, WM, WN, MT, (BM >= 256 ? 2 : 1), SMEM, EK>(g, e, acc, smem, m0, n0, ks, wm, wn, lane);
 }
 
@@ -997,7 +916,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_ring_kernel(GemmArgs g, 
   const int wm = wave % WM, wn = wave / WM;
 
   int tm, tn, ks = 0;
-  if (gridDim.y > 1 && !(g.dbg & 16)) split_tile_of(g.tiles_m, g.tiles_n, tm, tn, ks);  // dbg 16: A/B
+  if (gridDim.y > 1) split_tile_of(g.tiles_m, g.tiles_n, tm, tn, ks);
   else {
     tile_of(blockIdx.x, g.tiles_m, g.tiles_n, tm, tn);
     ks = blockIdx.y;
@@ -1110,15 +1029,6 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_ring_kernel(GemmArgs g, 
 template <bool AKC, bool BKC, int EK = EPI_GEN>
 __global__ __launch_bounds__(256, 2) void gemm_pp_kernel(GemmArgs g, EpiArgs e) {
   typedef f32x4 AccT;
-#ifdef FER_GEMM_EXP
-  // experiments library only: start one of the two workgroups of a CU (dbg 64: blocks 256..511 of the
-  // first dispatch round; dbg 128: odd blocks of it) (dbg >> 8) k cycles late, so that the pair runs
-  // its main loops and epilogues out of phase; the slot keeps that offset for its later blocks
-  if (blockIdx.x < 512 && (((g.dbg & 64) && blockIdx.x >= 256) || ((g.dbg & 128) && (blockIdx.x & 1)))) {
-    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
-    while (__builtin_amdgcn_s_memtime() - t0 < (unsigned long long)(g.dbg >> 8) * 1024ull) __builtin_amdgcn_s_sleep(8);
-  }
-#endif
   constexpr int BM = 256, BN = 128, WM = 2, WN = 2, MT = 16, RBK = 32, NST = 3, NW = 4;
   constexpr int TM = BM / WM, TN = BN / WN, FM = TM / MT, FN = TN / MT;
   constexpr int A_BYTES = BM * RBK * 2, B_BYTES = BN * RBK * 2, STAGE = A_BYTES + B_BYTES;
@@ -1127,7 +1037,7 @@ __global__ __launch_bounds__(256, 2) void gemm_pp_kernel(GemmArgs g, EpiArgs e) 
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave % WM, wn = wave / WM;
   int tm, tn, ks = 0;
-  if (gridDim.y > 1 && !(g.dbg & 16)) split_tile_of(g.tiles_m, g.tiles_n, tm, tn, ks);  // dbg 16: A/B
+  if (gridDim.y > 1) split_tile_of(g.tiles_m, g.tiles_n, tm, tn, ks);
   else {
     tile_of(blockIdx.x, g.tiles_m, g.tiles_n, tm, tn);
     ks = blockIdx.y;
@@ -1186,8 +1096,7 @@ static int launch_pp(GemmArgs g, const EpiArgs& e, hipStream_t st) {
   g.tiles_n = (g.N + 127) / 128;
   const dim3 grid(g.tiles_m * g.tiles_n, g.splits);
   // fixed-flag epilogue kinds as in the 8-phase kernel (K-contiguous operands, no split-K)
-  static const bool gen_only = getenv("FERVIT_EPI_GENERIC") != nullptr;
-  const int ek = (AKC && BKC && !g.partial && !gen_only) ? epi_kind(e) : EPI_GEN;
+  const int ek = (AKC && BKC && !g.partial) ? epi_kind(e) : EPI_GEN;
 #define FER_PPK(K) hipLaunchKernelGGL((gemm_pp_kernel<AKC, BKC, K>), grid, dim3(256), 0, st, g, e)
   if constexpr (AKC && BKC) {
     switch (ek) {
@@ -1315,17 +1224,9 @@ FER_DEV void tile_8ph(const GemmArgs& g, const EpiArgs& e, int bid, char* smem, 
   FER_STAMP(0);
 
   int tm, tn;
-#ifdef FER_GEMM_EXP
-  // experiments library: row-group size of the tile order (dbg bits 22-23: 8, 4, 16, 32)
-  {
-    const int gs = (g.dbg >> 22) & 3;
-    tile_of(bid, g.tiles_m, g.tiles_n, tm, tn, gs == 0 ? 8 : (gs == 1 ? 4 : (gs == 2 ? 16 : 32)));
-  }
-#else
   // GELU-gate fc1 forward: row groups of 4 tiles (377 -> 367-370 us alone, profiles/r03w_tile_group_ab.txt;
-  // the other kinds gain nothing from it); g.dbg bit 24 (FERVIT_GEMM_DBG) keeps 8 (A/B)
-  tile_of(bid, g.tiles_m, g.tiles_n, tm, tn, (EK == EPI_GATE && !(g.dbg & (1 << 24))) ? 4 : 8);
-#endif
+  // the other kinds gain nothing from it)
+  tile_of(bid, g.tiles_m, g.tiles_n, tm, tn, EK == EPI_GATE ? 4 : 8);
   const int m0 = tm * 256, n0 = tn * 256;
   const int ks = blockIdx.y;
   const int kbeg = ks * g.k_chunk;
@@ -1372,14 +1273,6 @@ FER_DEV void tile_8ph(const GemmArgs& g, const EpiArgs& e, int bid, char* smem, 
   if (claim_slot && tid == 0) *claim_slot = claimed;
   FER_STAMP(1);
 
-#ifdef FER_GEMM_EXP
-  // experiments library: static priority instead of the per-segment raise (dbg bit 20: waves 4-7
-  // at priority 1 for the whole main loop; bit 21: waves 0-3)
-  const bool sprio = g.dbg & (3 << 20);
-  if (sprio && ((g.dbg & (1 << 20)) ? wr : !wr)) __builtin_amdgcn_s_setprio(1);
-#else
-  constexpr bool sprio = false;
-#endif
   for (int T = 0; T < nk; ++T) {
     const bool n1 = T + 1 < nk, n2 = T + 2 < nk;
 #pragma unroll
@@ -1417,7 +1310,7 @@ FER_DEV void tile_8ph(const GemmArgs& g, const EpiArgs& e, int bid, char* smem, 
       (void)dummy;
       const int qm = (q == 0 || q == 2) ? 0 : 1;
       const int qn = (q == 0 || q == 3) ? 0 : 1;
-      if (!sprio) __builtin_amdgcn_s_setprio(1);
+      __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int kk = 0; kk < KS; ++kk)
 #pragma unroll
@@ -1425,20 +1318,15 @@ FER_DEV void tile_8ph(const GemmArgs& g, const EpiArgs& e, int bid, char* smem, 
 #pragma unroll
           for (int i = 0; i < QI; ++i)
             acc[qn * QI + i][qm * QJ + j] = mfma<MT>(fb[qn][kk][i], fa[qm][kk][j], acc[qn * QI + i][qm * QJ + j]);
-      if (!sprio) __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_s_setprio(0);
       __builtin_amdgcn_sched_barrier(0);
       if (T < 16) FER_STAMP(st_i + 3);
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
     }
   }
-  if (sprio) __builtin_amdgcn_s_setprio(0);
   if (nk > 0 && !wr) __builtin_amdgcn_s_barrier();  // waves 0-3 catch up with the stagger
   FER_STAMP(2);
-  if (g.dbg & 4) {  // timing experiment: no epilogue (keep the MFMAs alive)
-    if (acc[0][0][0] == 12345.f) g.ws[0] = 1.f;
-    return;
-  }
   static_assert(64 * (256 + 4) * 4 <= 2 * BUF, "epilogue staging (2 chunks per half) must fit");
   tile_epilogue<256, 256, 2, 4, MT, 2, 2 * BUF, EK>(g, e, acc, smem, m0, n0, ks, wr, wc, lane);
   FER_STAMP(3);
@@ -1462,14 +1350,6 @@ template <bool AKC, bool BKC, int MT, bool DYN, int EK>
 __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmArgs g, EpiArgs e) {
   __shared__ __attribute__((aligned(1024))) char smem[8 * 16384 + 16];
   const int ntiles = g.tiles_m * g.tiles_n;
-#ifdef FER_GEMM_EXP
-  // experiments library only (dbg & 64): workgroups with an odd (blockIdx.x / 8) start (dbg >> 8) k
-  // cycles late, so that the two halves of every XCD reach their tile epilogues at different times
-  if ((g.dbg & 64) && ((blockIdx.x >> 3) & 1)) {
-    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
-    while (__builtin_amdgcn_s_memtime() - t0 < (unsigned long long)(g.dbg >> 8) * 1024ull) __builtin_amdgcn_s_sleep(8);
-  }
-#endif
   if constexpr (!DYN) {
 #pragma unroll 1
     for (int bid = blockIdx.x; bid < ntiles; bid += gridDim.x) {
@@ -1725,8 +1605,7 @@ static int launch_bf16(GemmArgs g, const EpiArgs& e, hipStream_t st) {
   // the 128^2 K-contiguous MT16 kernel (the small-grid configs: w+ latents, 48 px) also gets the
   // fixed-flag epilogues (row operands through its LDS-DMA staging: the LDS-DMA kinds)
   if constexpr (BM == 128 && (BN == 128 || BN == 64) && AKC && BKC && MT == 16) {
-    static const bool gen_only = getenv("FERVIT_EPI_GENERIC") != nullptr;
-    int ek = (g.partial || gen_only) ? EPI_GEN : epi_kind(e);
+    int ek = g.partial ? EPI_GEN : epi_kind(e);
     if (ek == EPI_RES2) ek = EPI_RES;
     if (ek == EPI_MUL2) ek = EPI_MUL;
     switch (ek) {
@@ -1764,23 +1643,19 @@ static int launch_8ph(GemmArgs g, const EpiArgs& e, hipStream_t st) {
       n = 256;
     return n > 0 ? n : 256;
   }();
-  static const bool persist = getenv("FERVIT_GEMM_NOPERSIST") == nullptr;  // A/B switch
-  // FERVIT_GEMM_PERSIST_WG: persistent grid size (tuning runs; default one workgroup per CU)
-  static const int pwg = getenv("FERVIT_GEMM_PERSIST_WG") ? atoi(getenv("FERVIT_GEMM_PERSIST_WG")) : ncu;
+  // persistent grid: one workgroup per CU (a multiple of 8: the XCD-aware tile order)
   const int ntiles = g.tiles_m * g.tiles_n;
-  const int gx = persist ? std::min(ntiles, std::max(8, pwg / 8 * 8)) : ntiles;
+  const int gx = std::min(ntiles, std::max(8, ncu / 8 * 8));
   g.tq = nullptr;
   WqArgs w{};
-  if (persist && !fixed_stride_mode() && g.splits == 1) {
+  if (!fixed_stride_mode() && g.splits == 1) {
     w = wq_prepare_here(st, gx, ntiles);
     g.tq = w.q;
     for (int c = 0; c < 8; ++c) g.tq_base[c] = w.base[c];
   }
   dim3 grid(gx, g.splits);
-  // fixed-flag epilogues for the K-contiguous MT16 kernel (the forward and transposed-shadow dgrad
-  // path); FERVIT_EPI_GENERIC=1 keeps the generic one (A/B switch)
-  static const bool gen_only = getenv("FERVIT_EPI_GENERIC") != nullptr;
-  const int ek = (AKC && BKC && MT == 16 && !g.partial && !gen_only) ? epi_kind(e) : EPI_GEN;
+  // fixed-flag epilogues for the K-contiguous MT16 kernel (the forward and transposed-shadow dgrad path)
+  const int ek = (AKC && BKC && MT == 16 && !g.partial) ? epi_kind(e) : EPI_GEN;
 #define FER_8PH(DY, K) hipLaunchKernelGGL((gemm_8ph_kernel<AKC, BKC, MT, DY, K>), grid, dim3(512), 0, st, g, e)
 #define FER_8PH_K(DY)                                  \
   if constexpr (AKC && BKC && MT == 16) {              \
@@ -1831,15 +1706,9 @@ static bool use_128x64(long t128, long t64, int K) {
   return fill(t64, 3L * ncu) > fill(t128, 2L * ncu) + (K < 1024 ? 0.15 : 0.0);
 }
 
-static int g_forced_cfg = -2;  // -2: read FERVIT_GEMM_CFG once; -1: automatic
+static int g_forced_cfg = -1;  // fer_gemm_set_config; -1: automatic
 
-static int forced_cfg() {
-  if (g_forced_cfg == -2) {
-    const char* s = getenv("FERVIT_GEMM_CFG");
-    g_forced_cfg = s ? atoi(s) : -1;
-  }
-  return g_forced_cfg;
-}
+static int forced_cfg() { return g_forced_cfg; }
 
 // Tile configuration: 0..3 double-buffered (256^2 MT32, 256^2 MT16, 128^2 MT32, 128^2 MT16),
 // 4..7 BK=32 ring (same order), 8/9 the 8-phase 256^2 kernel (MT16 / MT32), 10 the ping-pong
@@ -1871,11 +1740,6 @@ int gemm_launch(const GemmDesc& d, const EpiArgs& e_in, hipStream_t st) {
   GemmArgs g{};
   g.A = d.A; g.B = d.B; g.lda = d.lda; g.ldb = d.ldb;
   g.M = d.M; g.N = d.N; g.K = d.K;
-  static const int dbg = getenv("FERVIT_GEMM_DBG") ? atoi(getenv("FERVIT_GEMM_DBG")) : 0;
-  g.dbg = dbg;
-#ifdef FER_GEMM_EXP
-  if (dbg & 32) e.colsum_accumulate |= 0x100;  // experiments library: epilogue without output stores
-#endif
   if (d.M <= 0 || d.N <= 0) return 0;
   if (d.N % 4) return set_error("gemm: N must be a multiple of 4");
   if (e.colsum && (!d.ws || d.ws_bytes < fer_gemm_colsum_ws(d.M, d.N)))
@@ -1922,28 +1786,21 @@ int gemm_launch(const GemmDesc& d, const EpiArgs& e_in, hipStream_t st) {
     if (max_splits < 2 || d.K < 1024 || tiles >= target) return 1;
     return (int)std::max<long>(1, std::min<long>({target / tiles, d.K / 256, (long)max_splits}));
   };
-  // split targets (workgroups per launch) of the 256^2 / 128^2 tile configs; FERVIT_GEMM_SPLIT_T256 /
-  // FERVIT_GEMM_SPLIT_T128 override them (tuning runs only)
+  // split targets (workgroups per launch) of the 256^2 / 128^2 tile configs
   // (MN x MN weight gradients: 192 workgroups, not one per CU -- they run beside the compute stream,
   // and leaving it CUs took the ViT-B step 36.06-36.33 -> 35.81-36.02 ms; 128 is 39 ms: the last
   // layers' weight gradients then form a long tail; profiles/r03aa_wgrad_split_target_ab.txt)
-  static const long tgt256 = getenv("FERVIT_GEMM_SPLIT_T256") ? atol(getenv("FERVIT_GEMM_SPLIT_T256")) : 256;
-  static const long tgt256_mn = getenv("FERVIT_GEMM_SPLIT_T256") ? tgt256 : 192;
+  constexpr long tgt256 = 256, tgt256_mn = 192;
   // (128^2, K-contiguous: split only below half a round; the ordered slab reduction costs more than the
   // idle CUs of an unsplit 152-228 tile grid -- latent fc2 fwd 50.7 -> 29.4 us, qkv dgrad 46.4 -> 22.9 us)
-  static const long tgt128 = getenv("FERVIT_GEMM_SPLIT_T128") ? atol(getenv("FERVIT_GEMM_SPLIT_T128")) : 512;
-  static const bool t128_env = getenv("FERVIT_GEMM_SPLIT_T128") != nullptr;
-  const long tgt128k = t128_env ? tgt128 : ((d.a_kc && d.b_kc) ? 256 : 512);
-  static const bool wg_mt32 = getenv("FERVIT_WGRAD_MT32") != nullptr;  // A/B switch, see below
+  const long tgt128k = (d.a_kc && d.b_kc) ? 256 : 512;
   int cfg = forced_cfg();
   if (cfg < 0) {
     if (d.K >= 8192 || t256 >= 256)  // big grids, and token-long weight gradients (split-K fills the GPU)
       // (MN x MN weight gradients split >= 16 ways -- out_proj / patch embed, 9 tiles x 28 splits --
       // run 97.7 -> 74.1 us alone on the MT32 ring, but the ViT-B step got 0.1-0.3 ms SLOWER with
-      // it on the weight-gradient stream (profiles/r03x_*, r03z_*): opt-in, FERVIT_WGRAD_MT32=1)
-      cfg = t256 * splits_for(t256, tgt256) >= 128
-                ? (!d.a_kc && !d.b_kc ? (splits_for(t256, tgt256_mn) >= 16 && wg_mt32 ? 4 : 5) : 8)
-                : 3;
+      // it on the weight-gradient stream (profiles/r03x_*, r03z_*): the MT16 ring stays)
+      cfg = t256 * splits_for(t256, tgt256) >= 128 ? (!d.a_kc && !d.b_kc ? 5 : 8) : 3;
     else if (d.a_kc && d.b_kc && t128 >= 128 && use_128x64(t128, (long)((d.M + 127) / 128) * ((d.N + 63) / 64), d.K))
       // 128x64 tiles (three workgroups per CU) where they fill the rounds better: latent fc2 fwd /
       // fc1 dgrad (152 tiles of 128^2, K 2048) 28.5 / 27.4 -> 25.4 / 24.3 us, fc1 fwd (608 tiles)
@@ -1961,23 +1818,6 @@ int gemm_launch(const GemmDesc& d, const EpiArgs& e_in, hipStream_t st) {
   g.cs_part = e.colsum ? reduction_ws(d.ws, (size_t)((d.M + (cfg_is_256(cfg) ? 255 : 127)) / (cfg_is_256(cfg) ? 256 : 128)) * d.N * 4,
                                       d.N, st)
                        : nullptr;
-  g.cnt = nullptr;
-  // in-launch split-K reduction (tile_epilogue; tickets after the slabs in the workspace, zeroed
-  // here) only with FERVIT_SPLITK_INLAUNCH=1: measured slower than the separate full-chip
-  // splitk_reduce launch -- the last split of a tile reads every slab of it alone on one CU
-  // (ViT-B fc1 wgrad 263 -> 310 us, step 36.3 -> 38.6 ms; latent 3-way split fc2 fwd 40 -> 55 us;
-  // profiles/r03q_splitk_inlaunch_ab.txt). The grouped weight gradients keep their in-launch
-  // reduction: two 64 KB slabs per tile there.
-  static const bool inlaunch = getenv("FERVIT_SPLITK_INLAUNCH") != nullptr;
-  if (g.partial && inlaunch) {
-    const long tiles = t128;  // >= the tile count of every configuration (tiles are >= 128 x 128)
-    const long slab_bytes = (long)g.splits * d.M * d.N * 4;
-    if (slab_bytes + tiles * 4 <= d.ws_bytes && slab_bytes < 0x7FFFFFF0L) {
-      g.cnt = (unsigned*)((char*)d.ws + slab_bytes);
-      if (hipMemsetAsync(g.cnt, 0, (size_t)tiles * 4, st) != hipSuccess) return set_error("gemm: ticket memset failed");
-    }
-  }
-
   if (d.a_kc && d.b_kc) dispatch_tile<true, true>(cfg, g, e, st);
   else if (d.a_kc && !d.b_kc) dispatch_tile<true, false>(cfg, g, e, st);
   else if (!d.a_kc && !d.b_kc) dispatch_tile<false, false>(cfg, g, e, st);
@@ -1989,7 +1829,7 @@ int gemm_launch(const GemmDesc& d, const EpiArgs& e_in, hipStream_t st) {
                 nullptr, st);
     rc = hip_check("gemm_colsum_reduce");
   }
-  if (rc || !g.partial || g.cnt) return rc;
+  if (rc || !g.partial) return rc;
   const long work = (long)d.M * (d.N / 4);
   const int blocks = (int)std::min<long>((work + 255) / 256, 4096);
   hipLaunchKernelGGL(splitk_reduce_kernel<bf16>, dim3(blocks), dim3(256), 0, st, d.ws, g.splits, (long)d.M,
@@ -2001,8 +1841,6 @@ int gemm_launch(const GemmDesc& d, const EpiArgs& e_in, hipStream_t st) {
 namespace {
 int wg_splits(int tiles, int K, int req) {
   if (req > 0) return std::min(req, 8);
-  static const int env = getenv("FERVIT_WG_SPLITS") ? atoi(getenv("FERVIT_WG_SPLITS")) : 0;  // tuning runs
-  if (env > 0) return std::min(env, 8);
   int dev = 0, ncu = 256;
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     ncu = 256;
@@ -2068,16 +1906,7 @@ extern "C" int fer_wgrad_group(const fer_wgrad_item* items, int n, int splits, f
   // interleave), K split to ~2 workgroups per CU. Latent-ViT layer (4 weights, 192 tiles, K 4864):
   // 57 us vs 74-77 us for the 4-slot ring (one workgroup per CU) with 4 or 8 waves at any split,
   // and 189 us as four split-K launches (profiles/r03o_wgrad_group_variants.txt).
-  // FERVIT_WG_VARIANT (tuning runs): 1 = 8 waves 4-slot, 2 = 8 waves 2-slot, 4 = 4 waves 4-slot.
-  static const int var = getenv("FERVIT_WG_VARIANT") ? atoi(getenv("FERVIT_WG_VARIANT")) : 0;
-  if (var == 1)
-    hipLaunchKernelGGL((gemm_wgrad_group_kernel<4, 4>), dim3(tile0, S), dim3(512), 0, st, g);
-  else if (var == 2)
-    hipLaunchKernelGGL((gemm_wgrad_group_kernel<2, 4>), dim3(tile0, S), dim3(512), 0, st, g);
-  else if (var == 4)
-    hipLaunchKernelGGL((gemm_wgrad_group_kernel<4, 2>), dim3(tile0, S), dim3(256), 0, st, g);
-  else
-    hipLaunchKernelGGL((gemm_wgrad_group_kernel<2, 2>), dim3(tile0, S), dim3(256), 0, st, g);
+  hipLaunchKernelGGL((gemm_wgrad_group_kernel<2, 2>), dim3(tile0, S), dim3(256), 0, st, g);
   return hip_check("wgrad_group");
 }
 

@@ -374,10 +374,9 @@ __global__ __launch_bounds__(256) void ln_part_reduce_kernel(const float* __rest
 
 // One round of workgroups: two per CU (the kernel runs two waves per SIMD), each walking its rows
 // with the grid stride. 1024 blocks (two rounds) measured 71.5 us at ViT-B vs 63.5 us: the second
-// round's tail and twice the column partials for part_reduce. FERVIT_LN_BWD_BLOCKS overrides (A/B).
+// round's tail and twice the column partials for part_reduce.
 static int ln_bwd_blocks(int M) {
   static const int cap = [] {
-    if (const char* v = getenv("FERVIT_LN_BWD_BLOCKS")) return std::max(1, atoi(v));
     int dev = 0, n = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
@@ -401,12 +400,10 @@ extern "C" int fer_layernorm_fwd(int dtype, const void* x, int64_t ldx, const fl
   if (gamma_rows < 1) gamma_rows = 1;
   if (row_div < 1) row_div = 1;
   dim3 grid(ceil_div(M, 4));
-  static const bool old_ln = getenv("FERVIT_LN_OLD") != nullptr;  // A/B switch
-  if (dtype == FER_BF16 && D % 8 == 0 && ldx % 8 == 0 && ldy % 8 == 0 && !old_ln) {
+  if (dtype == FER_BF16 && D % 8 == 0 && ldx % 8 == 0 && ldy % 8 == 0) {
     // one round of workgroups (four per CU at this kernel's 4 waves per SIMD): 25.8 us at ViT-B vs
-    // 27.7 us with 2048 (two rounds); FERVIT_LN_FWD_BLOCKS overrides (A/B)
+    // 27.7 us with 2048 (two rounds)
     static const int fcap = [] {
-      if (const char* v = getenv("FERVIT_LN_FWD_BLOCKS")) return std::max(1, atoi(v));
       int dev = 0, n = 0;
       if (hipGetDevice(&dev) != hipSuccess ||
           hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
@@ -453,11 +450,8 @@ extern "C" int fer_layernorm_bwd(int dtype, const void* dy, int64_t lddy, const 
   if (want && (!ws || ws_bytes < fer_layernorm_bwd_ws(M, D))) return set_error("layernorm_bwd: workspace too small");
   hipStream_t st = (hipStream_t)stream;
   if (want) ws = reduction_ws(ws, (size_t)fer_layernorm_bwd_ws(M, D), 3 * D, st);
-  static const bool old_ln = getenv("FERVIT_LN_OLD") != nullptr;  // A/B switch
-  if (dtype == FER_BF16 && D % 8 == 0 && lddy % 8 == 0 && ldx % 8 == 0 && lddx % 8 == 0 && (!res || ldr % 8 == 0) &&
-      !old_ln) {
-    static const bool g_rows = getenv("FERVIT_LN_BWD_GROWS") != nullptr;  // A/B: gamma loaded per row
-    const bool g1 = gamma_rows <= 1 && !g_rows;
+  if (dtype == FER_BF16 && D % 8 == 0 && lddy % 8 == 0 && ldx % 8 == 0 && lddx % 8 == 0 && (!res || ldr % 8 == 0)) {
+    const bool g1 = gamma_rows <= 1;  // gamma held in registers for the whole row loop
 #define FER_LN_BWD8(C)                                                                                          \
   if (g1) FER_LN_BWD8K((ln_bwd8_kernel<C, true>))                                                               \
   else FER_LN_BWD8K((ln_bwd8_kernel<C, false>))

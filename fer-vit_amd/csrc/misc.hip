@@ -4,6 +4,8 @@
 // LatentDecomposer projection, casts, dropout and the fused AdamW optimizer.
 // All cross-row reductions are two-pass (per-block partials, then a fixed-order sum),
 // so every result is bitwise reproducible run to run.
+#include <mutex>
+
 #include "common.h"
 #include "fervit_internal.h"
 
@@ -109,8 +111,12 @@ __global__ __launch_bounds__(256) void part_reduce_multi_kernel(const RedBatch b
     if (o) o[col] = d.accumulate ? o[col] + t : t;
   }
 }
+// One window per process, on one device (fer_reduce_defer rejects a second device while open); the
+// state is guarded by g_red_mu (part_reduce / reduction_ws are reached from every host entry point).
+static std::mutex g_red_mu;
 static struct {
   bool on = false, take = false;  // window open (queue valid) / taking new reductions
+  int dev = -1;
   char* arena = nullptr;
   size_t cap = 0, used = 0;
   hipStream_t st = nullptr;
@@ -127,13 +133,14 @@ static int red_flush() {
   g_red.used = 0;
   return hip_check("reduce_flush");
 }
-// Only partial sets up to FERVIT_REDUCE_MAX_KB (default 2 MB) are deferred: the small-token
+// Only partial sets up to 2 MB are deferred: the small-token
 // configurations' (latent w+ 1.5-1.9 MB per LayerNorm / attention bias) gain one launch each
 // (latent ViT 2.22 -> 2.16 ms), while ViT-B's (4.7-16.5 MB, 52 per step) measured 35.62 -> 35.75
 // ms deferred (their sums then re-read from HBM at the end of the backward instead of from the
 // last-level cache right after the producer; profiles/r03am_reduce_defer_ab.txt).
 float* reduction_ws(float* ws, size_t bytes, int ncols, hipStream_t st) {
-  static const size_t max_b = (getenv("FERVIT_REDUCE_MAX_KB") ? atol(getenv("FERVIT_REDUCE_MAX_KB")) : 2048) * 1024L;
+  constexpr size_t max_b = 2048 * 1024L;
+  std::lock_guard<std::mutex> lk(g_red_mu);
   if (!g_red.take || st != g_red.st || !red_batchable(ncols) || bytes > g_red.cap || bytes > max_b) return ws;
   bytes = (bytes + 255) & ~(size_t)255;
   if (g_red.used + bytes > g_red.cap || g_red.b.n == kRedMax) red_flush();
@@ -144,12 +151,27 @@ float* reduction_ws(float* ws, size_t bytes, int ncols, hipStream_t st) {
 
 void part_reduce(const float* part, int nb, long ld, int ncols, int seg, float* o0, float* o1, float* o2,
                  int accumulate, const float* scale, hipStream_t st) {
+  std::lock_guard<std::mutex> lk(g_red_mu);
   const bool in_arena = g_red.take && st == g_red.st && (const char*)part >= g_red.arena &&
                         (const char*)part < g_red.arena + g_red.cap;
-  bool dup = false;  // an output already queued: keep the two updates in stream order
+  // an output range overlapping a queued one (any base pointer: segmented o0/o1/o2 outputs vs a
+  // whole-buffer output): run the queue first, keeping the two updates in stream order
+  auto span = [](float* const (&o)[3], int k, int ncols, int seg) -> std::pair<const float*, const float*> {
+    const int n = std::min(seg, ncols - k * seg);
+    return o[k] && n > 0 ? std::make_pair((const float*)o[k], (const float*)o[k] + n)
+                         : std::make_pair((const float*)nullptr, (const float*)nullptr);
+  };
+  float* const mine[3] = {o0, o1, o2};
+  bool dup = false;
   for (int i = 0; i < g_red.b.n && !dup; ++i)
-    for (int k = 0; k < 3; ++k)
-      for (float* o : {o0, o1, o2}) dup |= o && g_red.b.d[i].o[k] == o;
+    for (int k = 0; k < 3 && !dup; ++k) {
+      const auto q = span(g_red.b.d[i].o, k, g_red.b.d[i].ncols, g_red.b.d[i].seg);
+      if (!q.first) continue;
+      for (int j = 0; j < 3 && !dup; ++j) {
+        const auto m = span(mine, j, ncols, seg);
+        dup = m.first && m.first < q.second && q.first < m.second;
+      }
+    }
   if (in_arena && !scale && red_batchable(ncols) && g_red.b.n < kRedMax && !dup) {
     g_red.b.d[g_red.b.n++] = RedDesc{part, ld, {o0, o1, o2}, nb, ncols, seg, accumulate, g_red.blocks};
     g_red.blocks += ceil_div(ncols, 64);
@@ -943,11 +965,16 @@ int fer::set_step_ptr_misc(const uint64_t* p) { return set_step_ptr_here(p) == h
 extern "C" int64_t fer_colsum_ws(int M, int N) { return (int64_t)colsum_nblk(M) * N * 4; }
 
 extern "C" int fer_reduce_defer(int mode, void* arena, int64_t arena_bytes, fer_stream_t stream) {
+  std::lock_guard<std::mutex> lk(g_red_mu);
   if (mode == 2) {  // pause: keep the queue, stop taking new reductions
     g_red.take = false;
     return 0;
   }
   if (mode != 0 && mode != 1) return set_error("reduce_defer: mode must be 0, 1 or 2");
+  int dev = -1;
+  if (hipGetDevice(&dev) != hipSuccess) return set_error("reduce_defer: hipGetDevice failed");
+  if (mode == 1 && g_red.on && dev != g_red.dev)
+    return set_error("reduce_defer: a window is open on another device (one window per process)");
   const bool same = g_red.on && g_red.arena == (char*)arena && g_red.cap == (size_t)arena_bytes &&
                     g_red.st == (hipStream_t)stream;
   if (g_red.on && (mode == 0 || !same)) {
@@ -963,11 +990,15 @@ extern "C" int fer_reduce_defer(int mode, void* arena, int64_t arena_bytes, fer_
     g_red.st = (hipStream_t)stream;
     g_red.used = 0;
   }
+  g_red.dev = dev;
   g_red.on = g_red.take = true;
   return 0;
 }
 
-extern "C" int fer_reduce_flush(void) { return g_red.on ? red_flush() : 0; }
+extern "C" int fer_reduce_flush(void) {
+  std::lock_guard<std::mutex> lk(g_red_mu);
+  return g_red.on ? red_flush() : 0;
+}
 
 extern "C" int fer_colsum(int dtype, const void* x, int64_t ldx, int M, int N, float* out, int accumulate,
                           const float* scale_ptr, float* ws, int64_t ws_bytes, fer_stream_t stream) {

@@ -49,18 +49,14 @@ def load_checkpoint(path: str, model: Optional[torch.nn.Module] = None,
 
 
 def _safe_load(path: str):
-    """torch.load(weights_only=True) with the numpy reconstructors allow-listed: through the
-    `safe_globals` context manager where torch has it, else the process-wide
-    `add_safe_globals` (torch 2.4), else a plain weights_only load (older torch: tensor-only
-    checkpoints still load; numpy-valued metrics are then refused by torch, never unpickled)."""
+    """torch.load(weights_only=True) with the numpy reconstructors allow-listed through the
+    `safe_globals` context manager. Needs torch >= 2.5 (the reference pins 2.5.1,
+    `environment.yml:113`; fervit.module's always_call forward hooks need >= 2.1 as well)."""
     ser = torch.serialization
-    g = _numpy_safe_globals()
-    if hasattr(ser, "safe_globals"):
-        with ser.safe_globals(g):
-            return torch.load(path, map_location="cpu", weights_only=True)
-    if hasattr(ser, "add_safe_globals"):
-        ser.add_safe_globals(g)
-    return torch.load(path, map_location="cpu", weights_only=True)
+    if not hasattr(ser, "safe_globals"):
+        raise RuntimeError("fervit checkpoints need torch >= 2.5 (torch.serialization.safe_globals)")
+    with ser.safe_globals(_numpy_safe_globals()):
+        return torch.load(path, map_location="cpu", weights_only=True)
 
 
 def _numpy_safe_globals():

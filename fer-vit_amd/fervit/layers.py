@@ -81,20 +81,26 @@ class _ReduceDefer:
     autograd-engine callback), a gradient-ready hook (DDP buckets) or a full queue runs them as ONE
     launch. Bit-identical to the immediate reductions. Only the layer functions below open the
     window (they write gradients into the flat buffer, which nothing reads before the backward
-    ends); every other caller of the same ops keeps the immediate path. FERVIT_REDUCE_DEFER=0 turns
-    it off (A/B); FERVIT_REDUCE_ARENA_MB sizes the arena (default 64 MB; a full arena flushes) and
-    csrc FERVIT_REDUCE_MAX_KB the largest partial set it takes (default 2 MB: small-token configs)."""
+    ends); every other caller of the same ops keeps the immediate path. `enabled` turns it off (tests);
+    the arena is 64 MB (a full arena flushes) and csrc takes partial sets up to 2 MB (small-token
+    configs)."""
 
     def __init__(self):
-        self.enabled = os.environ.get("FERVIT_REDUCE_DEFER", "1") != "0"
-        self.mb = int(os.environ.get("FERVIT_REDUCE_ARENA_MB", "64"))
+        self.enabled = True
+        self.mb = 64
         self.arena: Optional[torch.Tensor] = None
         self.open = False
+        self.owner = -1  # autograd graph task whose end-of-backward callback closes the window
         self.windows = 0  # backward passes that deferred (tests)
 
     def begin(self, device) -> bool:
         if not self.enabled or device is None or device.type != "cuda":
             return False
+        task = torch._C._current_graph_task_id()
+        if self.open and task != self.owner:
+            # the window's backward ended without running its callback (torch drops queued
+            # callbacks when a backward raises): run what it queued, then open a fresh window
+            self._end()
         if not self.open:
             if self.arena is None or self.arena.device != device:
                 if torch.cuda.is_current_stream_capturing():
@@ -105,6 +111,7 @@ class _ReduceDefer:
             except RuntimeError:  # not inside a backward pass
                 return False
             self.open = True
+            self.owner = task
             self.windows += 1
         check(lib().fer_reduce_defer(1, self.arena.data_ptr(), self.arena.numel() * 4, ops.stream()), "reduce_defer")
         return True
@@ -118,7 +125,14 @@ class _ReduceDefer:
 
     def _end(self) -> None:
         self.open = False
+        self.owner = -1
         check(lib().fer_reduce_defer(0, None, 0, None), "reduce_defer")
+
+    def close_if_open(self) -> None:
+        """Readers of the gradients (optimizer step, clipping) outside a backward: a window still
+        open here lost its callback to an exception in its backward -- run its queued sums now."""
+        if self.open and torch._C._current_graph_task_id() == -1:
+            self._end()
 
 
 REDUCE = _ReduceDefer()
@@ -151,12 +165,9 @@ def _finish(flat: FlatParams, params, needs) -> None:
 
 
 def _wgrad(dy, x, out, **kw):
-    """dW (+)= dy^T x on the weight-gradient stream (runtime.WGRAD) (FERVIT_WGRAD_SINGLE_GROUP=1: a
-    plain one at a small token count as a grouped launch of one, see WGRAD_SINGLE_GROUP)."""
-    if (WGRAD_SINGLE_GROUP and set(kw) <= {"accumulate"} and dy.dtype == torch.bfloat16
-            and out.dtype == torch.float32 and dy.shape[0] <= WGRAD_GROUP_MAX_M):
-        acc = bool(kw.get("accumulate", False))
-        return WGRAD.run(lambda: ops.linear_wgrad_group([(dy, x, out, acc)]), dy, x)
+    """dW (+)= dy^T x on the weight-gradient stream (runtime.WGRAD). (Lone weight gradients as grouped
+    launches of one measured slower: hybrid 6.52-6.61 -> 6.84-6.88 ms, an adapter's 6-tile gradient gets
+    too few workgroups, profiles/r03af_single_wgrad_group_ab.txt.)"""
     return WGRAD.run(lambda: ops.linear_wgrad(dy, x, out, **kw), dy, x)
 
 
@@ -164,14 +175,7 @@ def _wgrad(dy, x, out, **kw):
 # its backward (csrc/gemm.hip gemm_wgrad_group_kernel) instead of one split-K GEMM (+ reduction)
 # each: the w+ latent (4,864 rows) and 48 px (640) configurations. ViT-B/16 (50,432 rows) keeps
 # the per-weight split-K launches, issued as soon as each dY exists.
-WGRAD_GROUP_MAX_M = int(os.environ.get("FERVIT_WGRAD_GROUP_MAX_M", "16384"))
-# A/B, opt-in (FERVIT_WGRAD_SINGLE_GROUP=1): lone weight gradients (input projections, adapters, 48 px
-# patch embed) as groups of one -- measured slower (hybrid 6.52-6.61 -> 6.84-6.88 ms: an adapter's
-# 6-tile gradient gets too few workgroups), profiles/r03af_single_wgrad_group_ab.txt
-WGRAD_SINGLE_GROUP = os.environ.get("FERVIT_WGRAD_SINGLE_GROUP", "0") == "1"
-# A/B: issue each weight gradient after the input-gradient GEMM that shares its dY instead of
-# before it (the weight-gradient stream then overlaps the next kernels of the chain)
-WGRAD_LATE = os.environ.get("FERVIT_WGRAD_LATE") == "1"
+WGRAD_GROUP_MAX_M = 16384
 
 
 class _WgradBatch:
@@ -253,37 +257,24 @@ class PostNormLayerFn(torch.autograd.Function):
         ops.layernorm_bwd(dout, z, m2, r2, n2w.data, dx=dz, dx_drop=dh2, dropout=pd, seed=seeds[3], dgamma=gn2w,
                           dbeta=gn2b, dbias=gb2, accumulate=acc)
         dh2 = dz if dh2 is None else dh2
-        late = WGRAD_LATE
-        if not late:
-            wb.add(dh2, g, gw2, acc)
+        wb.add(dh2, g, gw2, acc)
         # linear1.bias grad = column sums of dF, fused into this GEMM's epilogue
         dF = _dgrad(flat, dh2, w2, dt, aux=f, aux_act="mul", colsum=gb1, colsum_accumulate=acc)
-        if late:
-            wb.add(dh2, g, gw2, acc)
-        else:
-            wb.add(dF, x1, gw1, acc)
+        wb.add(dF, x1, gw1, acc)
         dx1 = _dgrad(flat, dF, w1, dt, res=dz)
-        if late:
-            wb.add(dF, x1, gw1, acc)
         # LN1 (+ dropout of the attention branch, + out_proj bias grad)
         dy = torch.empty_like(y)
         dhh = torch.empty_like(y) if pd > 0 else None
         ops.layernorm_bwd(dx1, y, m1, r1, n1w.data, dx=dy, dx_drop=dhh, dropout=pd, seed=seeds[1], dgamma=gn1w,
                           dbeta=gn1b, dbias=gout_b, accumulate=acc)
         dhh = dy if dhh is None else dhh
-        if not late:
-            wb.add(dhh, o, gout_w, acc)
+        wb.add(dhh, o, gout_w, acc)
         do = _dgrad(flat, dhh, out_w, dt)
-        if late:
-            wb.add(dhh, o, gout_w, acc)
         dqkv = _empty(M, 3 * D, x)
         ops.attention_bwd(qkv, o, do, lse, dqkv, cfg.B, cfg.N, cfg.H, dh, dropout=pd, seed=seeds[0], colsum=gin_b,
                           colsum_accumulate=acc)
-        if not late:
-            wb.add(dqkv, x, gin_w, acc)
+        wb.add(dqkv, x, gin_w, acc)
         dx = _dgrad(flat, dqkv, in_w, dt, res=dy)
-        if late:
-            wb.add(dqkv, x, gin_w, acc)
         wb.flush()
         _finish(flat, P, needs)
         ctx.saved = None

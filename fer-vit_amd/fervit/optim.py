@@ -188,6 +188,7 @@ class FusedAdamW(torch.optim.Optimizer):
         loss = closure() if closure is not None else None
         flat = self._bind()
         runtime.WGRAD.sync()  # weight gradients of the last backward (normally joined already)
+        _close_reduce_window()
         if self._frozen is not None:  # graph mode: static segments, device step counter
             dev, nseg, maxn = self._frozen
             half = flat.bf16()
@@ -221,6 +222,13 @@ class FusedAdamW(torch.optim.Optimizer):
         return coef
 
 
+def _close_reduce_window() -> None:
+    """Queued bias / LayerNorm gradient sums of a backward that raised (layers._ReduceDefer)."""
+    from .layers import REDUCE
+
+    REDUCE.close_if_open()
+
+
 def clip_grad_norm_(model, max_norm: float, sq_scale: float = 1.0, optimizer: Optional[FusedAdamW] = None
                     ) -> torch.Tensor:
     """torch.nn.utils.clip_grad_norm_ (`train/train_latent_vit_v2.py:133`) on the model's flat
@@ -235,6 +243,7 @@ def clip_grad_norm_(model, max_norm: float, sq_scale: float = 1.0, optimizer: Op
     zeroes such stale slots and copies foreign `.grad` tensors into the flat buffer first."""
     flat = model.fer_flat()
     runtime.WGRAD.sync()
+    _close_reduce_window()
     flat.settle_grads()
     out = torch.empty(2, dtype=torch.float32, device=flat.grad.device)
     ws = ops.WS.get(4 * 4096, flat.grad.device, slot=3)

@@ -237,16 +237,16 @@ class _WgradStream:
     before backward returns (optimizer, clipping and user code then see finished gradients).
     Under HIP-graph capture (StepGraph) the side stream forks from the capturing stream through
     the same event wait and is joined back by the same callback, so the captured graph keeps the
-    two branches -- with FERVIT_WGRAD_CAPTURE=1 only: measured on the graph-replayed configs
-    (r03m, one box) it did not pay (w+ latent ViT 3.07 -> 3.04 ms, hybrid 7.09 -> 7.22 ms, 48 px
-    ImageViT 1.65 -> 1.75 ms), so captured steps keep one branch by default. Off entirely with
-    FERVIT_WGRAD_STREAM=0 (same stream as the dgrads)."""
+    two branches -- with `in_capture` only: measured on the graph-replayed configs (r03m, one box)
+    it did not pay (w+ latent ViT 3.07 -> 3.04 ms, hybrid 7.09 -> 7.22 ms, 48 px ImageViT 1.65 ->
+    1.75 ms), so captured steps keep one branch. `enabled = False` puts the weight gradients on the
+    compute stream (the bench's isolated GEMM probe)."""
 
     def __init__(self):
         self.streams = {}
         self.join_queued = False
-        self.enabled = os.environ.get("FERVIT_WGRAD_STREAM", "1") != "0"
-        self.in_capture = os.environ.get("FERVIT_WGRAD_CAPTURE", "0") == "1"
+        self.enabled = True
+        self.in_capture = False
 
     def _off(self) -> bool:
         return not self.enabled or (not self.in_capture and torch.cuda.is_current_stream_capturing())

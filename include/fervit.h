@@ -165,7 +165,10 @@ int fer_colsum(int dtype, const void* x, int64_t ldx, int M, int N, float* out, 
  * fixed-order partial sum instead of launching it; mode 2 pauses (the queue stays, new calls run
  * immediately); mode 0 flushes and closes. fer_reduce_flush runs every queued sum as ONE launch on
  * that stream (bit-identical to the immediate path). Callers flush before anything reads those
- * gradients. Host state is per process (one window at a time). */
+ * gradients. Host state is per process (one window at a time, on one device: opening it from another
+ * device while open is an error). Only part_reduce writers (the entry points above) are ordered
+ * against the queue -- a queued sum runs first when a later reduction's output range overlaps its
+ * own; any OTHER kernel that writes a queued gradient inside the window must flush first. */
 int fer_reduce_defer(int mode, void* arena, int64_t arena_bytes, fer_stream_t stream);
 int fer_reduce_flush(void);
 

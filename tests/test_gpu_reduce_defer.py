@@ -145,3 +145,38 @@ def test_reduce_defer_c_api_contract():
         assert torch.equal(dg4, g_ref) and torch.equal(db4, b_ref)
     finally:
         check(lib().fer_reduce_defer(0, None, 0, None), "close")
+
+
+def test_deferred_window_after_backward_exception():
+    """A backward that raises drops its queued end-of-backward callback: the window it
+    opened must not swallow the next backward's sums. The next backward's gradients equal the
+    immediate path's, and an optimizer step / clip after the failed backward closes the window."""
+    from fervit.layers import REDUCE
+    from fervit.optim import clip_grad_norm_
+    from test_gpu_models import build
+
+    m, _ = build("latent_vit")
+    m.set_precision("bf16").train()
+    x, y = case_inputs("latent_vit")
+    x, y = x.cuda(), y.cuda()
+    ref = _grads(m, x, y, False)
+
+    def boom(_g):
+        raise RuntimeError("injected backward failure")
+
+    for after in ("backward", "clip"):
+        m.zero_grad(set_to_none=True)
+        xr = x.clone().requires_grad_(True)
+        xr.register_hook(boom)  # fires after every layer backward opened the window
+        loss = torch.nn.functional.cross_entropy(m(xr), y, label_smoothing=0.1)
+        with pytest.raises(RuntimeError, match="injected"):
+            loss.backward()
+        assert REDUCE.open  # its callback was dropped with the exception
+        if after == "clip":
+            clip_grad_norm_(m, 1.0)
+            assert not REDUCE.open
+        got = _grads(m, x, y, True)
+        assert not REDUCE.open
+        assert got.keys() == ref.keys()
+        for k in ref:
+            assert torch.equal(got[k], ref[k]), (after, k)

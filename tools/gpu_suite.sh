@@ -1,0 +1,25 @@
+# One GPU call: the -m gpu suite, then the default bench line, then a rocprofv3 kernel-trace summary of
+# a short bench run. usage: bash tools/gpu_suite.sh <tag> [tests|bench|prof ...]   (default: all three)
+set -o pipefail
+TAG=${1:-x}; shift
+STEPS=${*:-tests bench prof}
+cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out && export TMPDIR=/tmp
+for s in $STEPS; do
+  case $s in
+    tests)
+      timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 150 \
+        --timeout-method thread > gpurun_out/${TAG}_tests.txt 2>&1 || { tail -30 gpurun_out/${TAG}_tests.txt; exit 1; }
+      tail -2 gpurun_out/${TAG}_tests.txt ;;
+    bench)
+      timeout -k 10 400 python -u bench.py > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err \
+        || { tail -20 gpurun_out/${TAG}_bench.err; exit 1; }
+      cut -c1-400 gpurun_out/${TAG}_bench.json ;;
+    prof)
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_prof -o run -- \
+        python3 bench.py --steps 10 --warmup 5 --no-cpu-baseline --no-traffic > gpurun_out/${TAG}_prof.json 2>&1 \
+        || { tail -20 gpurun_out/${TAG}_prof.json; exit 1; }
+      f=$(find gpurun_out/${TAG}_prof -name "*kernel_stats.csv" | head -1)
+      python3 tools/prof_csv_summary.py "$f" 19 40 > gpurun_out/${TAG}_kernel_summary.txt 2>&1 || true
+      head -30 gpurun_out/${TAG}_kernel_summary.txt ;;
+  esac
+done
