@@ -332,12 +332,7 @@ __global__ __launch_bounds__(64 * (NB + 1)) void attn_fwd_pers(const bf16* __res
 #pragma unroll
       for (int s = 0; s < 4; ++s) kfr[s] = rd_row(Ki, lane & 31, 2 * s + hh);
       // softmax + dropout + P.V of key block kb, whose S^T is in st
-      auto block = [&](int kb, f32x16& st) {
-        bf16x8 vfr[2][2];
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-          for (int db = 0; db < 2; ++db) vfr[s2][db] = rd_tr(Vi, kb * 32 + 16 * s2, db * 32, lane);
+      auto block = [&](int kb, f32x16& st, const bf16x8 (&vfr)[2][2]) {
         if (kb == NB - 1 && NB * 32 > N) {  // only the last key block has padding keys
 #pragma unroll
           for (int r = 0; r < 16; ++r)
@@ -357,10 +352,12 @@ __global__ __launch_bounds__(64 * (NB + 1)) void attn_fwd_pers(const bf16* __res
           ot[1] *= al;
         }
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          st[r] = ex2(fmaf(st[r], sl2, -m));
-          l += st[r];
-        }
+        for (int r = 0; r < 16; ++r) st[r] = ex2(fmaf(st[r], sl2, -m));
+        // the block's row sum as a tree (four independent chains), not a 16-long dependent chain
+        float ls[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) ls[c] = (st[c] + st[c + 4]) + (st[c + 8] + st[c + 12]);
+        l += (ls[0] + ls[1]) + (ls[2] + ls[3]);
         if (thr) {
           const uint32_t p0 = (row >> 1) + kb * 16 + 2 * hh;  // hash pair of register 0
           uint64_t bal[16];
@@ -373,10 +370,8 @@ __global__ __launch_bounds__(64 * (NB + 1)) void attn_fwd_pers(const bf16* __res
             bal[r] = __builtin_amdgcn_ballot_w64(k0);
             bal[r + 1] = __builtin_amdgcn_ballot_w64(k1);
           }
-          if (mask) {
-            uint32_t word = 0;
-            word = wl_keys8<0>(word, bal);
-            word = wl_keys8<8>(word, bal + 8);
+          if (mask) {  // two independent writelane chains (lanes 0-15, 16-31)
+            const uint32_t word = wl_keys8<0>(0u, bal) | wl_keys8<8>(0u, bal + 8);
             if (lane < 32) mask[(((long)bh * NB + kb) * NB + w) * 32 + lane] = word;
           }
         }
@@ -387,17 +382,36 @@ __global__ __launch_bounds__(64 * (NB + 1)) void attn_fwd_pers(const bf16* __res
           for (int db = 0; db < 2; ++db) ot[db] = mfma32(vfr[s2][db], pf, ot[db]);
         }
       };
+      // Software-pipelined over key blocks: S^T of block kb+1 goes to the matrix pipe BEFORE the
+      // softmax / dropout VALU work of block kb, so the two overlap within the wave (the MFMA chain's
+      // latency was exposed at the head of every block); K fragments run two blocks ahead.
+      f32x16 st = {};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) st = mfma32(kfr[s], qf[s], st);
+      if (NB > 1) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) kfr[s] = rd_row(Ki, 32 + (lane & 31), 2 * s + hh);
+      }
 #pragma unroll 1
-        for (int kb = 0; kb < NB; ++kb) {
-          f32x16 st = {};
+      for (int kb = 0; kb < NB; ++kb) {
+        bf16x8 vfr[2][2];
 #pragma unroll
-          for (int s = 0; s < 4; ++s) st = mfma32(kfr[s], qf[s], st);
-          if (kb + 1 < NB) {
+        for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
-            for (int s = 0; s < 4; ++s) kfr[s] = rd_row(Ki, (kb + 1) * 32 + (lane & 31), 2 * s + hh);
+          for (int db = 0; db < 2; ++db) vfr[s2][db] = rd_tr(Vi, kb * 32 + 16 * s2, db * 32, lane);
+        f32x16 sn = {};
+        if (kb + 1 < NB) {
+#pragma unroll
+          for (int s = 0; s < 4; ++s) sn = mfma32(kfr[s], qf[s], sn);
+          if (kb + 2 < NB) {
+#pragma unroll
+            for (int s = 0; s < 4; ++s) kfr[s] = rd_row(Ki, (kb + 2) * 32 + (lane & 31), 2 * s + hh);
           }
-          block(kb, st);
         }
+        __builtin_amdgcn_sched_barrier(0);  // keep the next block's MFMAs ahead of this block's VALU
+        block(kb, st, vfr);
+        st = sn;
+      }
       l = xhalf_sum(l);
       if (q < N) {
         store_rows_q(out + ((long)b * N + q) * ldo + h * dh, ot[0], ot[1], dscale / l, hh, dh);

@@ -14,6 +14,13 @@ for s in $STEPS; do
       timeout -k 10 400 python -u bench.py > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err \
         || { tail -20 gpurun_out/${TAG}_bench.err; exit 1; }
       cut -c1-400 gpurun_out/${TAG}_bench.json ;;
+    attn|gemm|ln)
+      # A/B microbench: the in-tree library and fer-vit_amd/fervit/libfervit_base.so (if present), interleaved
+      for rep in 1 2; do for lib in libfervit.so libfervit_base.so; do
+        [ -f fer-vit_amd/fervit/$lib ] || continue
+        (cd tools && FERVIT_LIB=$GRAFT_REPO_ROOT/fer-vit_amd/fervit/$lib timeout -k 10 200 python -u ${s}_bench.py 2>&1 \
+          | grep -v amdgpu.ids | sed "s/^/[$lib] /") | tee -a gpurun_out/${TAG}_${s}_ab.txt || exit 1
+      done; done ;;
     prof)
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_prof -o run -- \
         python3 bench.py --steps 10 --warmup 5 --no-cpu-baseline --no-traffic > gpurun_out/${TAG}_prof.json 2>&1 \
