@@ -440,7 +440,8 @@ def main():
         opt.step()
         return loss
 
-    use_graph = args.graph == "on" or (args.graph == "auto" and args.config != "vit_base_224" and world == 1)
+    # (with N > 1 the captured step holds the RCCL bucket all-reduces too: fervit/ddp.py)
+    use_graph = args.graph == "on" or (args.graph == "auto" and args.config != "vit_base_224")
     for _ in range(args.warmup):
         step()
     if use_graph:
