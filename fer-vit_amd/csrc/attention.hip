@@ -58,8 +58,7 @@ FER_DEV bf16x8 rd_tr(const char* img, int rbase, int cb, int lane) {
   const char* a2 = img + r2 * 128 + ((c ^ swz(r2)) << 4) + half;
   short4_t t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4_t*)a1);
   short4_t t2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4_t*)a2);
-  bf16x4 b1 = __builtin_bit_cast(bf16x4, t1), b2 = __builtin_bit_cast(bf16x4, t2);
-  return bf16x8{b1[0], b1[1], b1[2], b1[3], b2[0], b2[1], b2[2], b2[3]};
+  return cat8(t1, t2);
 }
 
 FER_DEV bf16x8 pack8(const f32x16& a, int s) {
@@ -270,6 +269,35 @@ FER_DEV void fwd_load_q(bf16x8 (&qf)[4], const bf16* qkv, long ldq, int unit, in
   }
 }
 
+#ifdef FER_ATTN_STAMPS
+// Diagnostic build only: s_memtime stamps of workgroup 0, units 2..3, every wave (lane 0).
+__device__ unsigned long long g_ast[9][64];
+__device__ unsigned long long g_bst[8][128];
+#define BST(i)                                                                        \
+  do {                                                                                \
+    if (bst_on) {                                                                     \
+      unsigned long long t_;                                                          \
+      __builtin_amdgcn_sched_barrier(0);                                              \
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");       \
+      __builtin_amdgcn_sched_barrier(0);                                              \
+      if ((threadIdx.x & 63) == 0) g_bst[w][(i)] = t_;                                \
+    }                                                                                 \
+  } while (0)
+#define AST(i)                                                                        \
+  do {                                                                                \
+    if (st_on) {                                                                      \
+      unsigned long long t_;                                                          \
+      __builtin_amdgcn_sched_barrier(0);                                              \
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");       \
+      __builtin_amdgcn_sched_barrier(0);                                              \
+      if (lane == 0) g_ast[w][(i)] = t_;                                              \
+    }                                                                                 \
+  } while (0)
+#else
+#define AST(i) do {} while (0)
+#define BST(i) do {} while (0)
+#endif
+
 template <int NB>
 __global__ __launch_bounds__(64 * (NB + 1)) void attn_fwd_pers(const bf16* __restrict__ qkv, long ldq,
                                                                bf16* __restrict__ out, long ldo,
@@ -279,10 +307,36 @@ __global__ __launch_bounds__(64 * (NB + 1)) void attn_fwd_pers(const bf16* __res
   seed = step_seed(seed);
   constexpr int IMG = NB * 32 * 128;
   __shared__ __attribute__((aligned(1024))) char lds[4 * IMG + 16];  // 2 x (K image, V image), unit hand-off
-  volatile int* hand = (volatile int*)(lds + 4 * IMG);
+  lds_vint* hand = FER_LDS_INT(lds + 4 * IMG);
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), hh = lane >> 5;
   const u32x4 rs = rsrc4(qkv);
   const int q = w * 32 + (lane & 31);
+  // Every global access of the consumers is a buffer op with the out-of-range lanes at FER_OOB (dropped
+  // / zero-filled by the range check) instead of an exec-masked one: the compiler's vmcnt counts stay
+  // exact (with masked loads it flushed vmcnt(0) at the key-block loop's entry, i.e. waited for the
+  // next unit's Q prefetch before starting this unit). Per-lane offsets once; the unit part is the
+  // scalar offset.
+  const __amdgpu_buffer_rsrc_t rq = make_rsrc(qkv), ro = make_rsrc(out), rl = make_rsrc(lse),
+                               rmk = make_rsrc(mask ? (const void*)mask : (const void*)lse);
+  uint32_t q_off[4], o_off[8];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int d0 = 16 * s + 8 * hh;
+    q_off[s] = (q < N && d0 < dh) ? (uint32_t)(((long)q * ldq + d0) * 2) : FER_OOB;
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int d = (i >> 2) * 32 + 8 * (i & 3) + 4 * hh;
+    o_off[i] = (q < N && d < dh) ? (uint32_t)(((long)q * ldo + d) * 2) : FER_OOB;
+  }
+  const uint32_t lse_off = (q < N && hh == 0) ? (uint32_t)(q * 4) : FER_OOB;
+  const uint32_t mk_off = (mask && lane < 32) ? (uint32_t)(lane * 4) : FER_OOB;
+  auto load_q = [&](bf16x8 (&qv)[4], int unit) {
+    const int b = unit / H, h = unit - b * H;
+    const int so = __builtin_amdgcn_readfirstlane((int)((((long)b * N) * ldq + h * dh) * 2));
+#pragma unroll
+    for (int s = 0; s < 4; ++s) qv[s] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rq, q_off[s], so, 0));
+  };
   // units: fixed stride, or the work queue `wq` (common.h): the first unit is blockIdx.x, the next
   // one is claimed at the start, then the producer's lane 0 claims the unit after next while this
   // one runs and hands it on through hand[k & 1] at the unit's last barrier
@@ -297,33 +351,44 @@ __global__ __launch_bounds__(64 * (NB + 1)) void attn_fwd_pers(const bf16* __res
   }
   bf16x8 qf[4];
   if (w == NB) {
+    uint32_t c0 = 0;
+    if (wq.q && claimer) c0 = wq_claim_issue(wq.q);  // its round trip overlaps the DMA wait
     fwd_dma_unit<NB>(lds, rs, u, ldq, N, H, dh, lane);
-    int c0 = -1;
-    if (wq.q && claimer) c0 = wq_claim(wq.q, wq.base, BH);  // its round trip overlaps the DMA wait
     wait_vm<0>();
-    if (wq.q && claimer) hand[2] = c0;
+    asm volatile("" : "+v"(c0));
+    if (wq.q && claimer) hand[2] = wq_claim_finish(c0, wq.base, BH);
   } else {
-    fwd_load_q(qf, qkv, ldq, u, N, H, dh, q, hh);
+    load_q(qf, u);
   }
   bar_lds();
   if (wq.q) un = __builtin_amdgcn_readfirstlane(hand[2]);
 #pragma unroll 1
   for (int k = 0;; ++k) {
+#ifdef FER_ATTN_STAMPS
+    const bool st_on = blockIdx.x == 0 && (k == 2 || k == 3);
+    const int sb = (k - 2) * 32;
+#endif
+    AST(sb + 0);
     if (w == NB) {
       int unn = -1;
+      uint32_t craw = 0;
       if (wq.q) {
-        if (claimer && un >= 0) unn = wq_claim(wq.q, wq.base, BH);
+        if (claimer && un >= 0) craw = wq_claim_issue(wq.q);
       } else if (un >= 0 && un + (int)gridDim.x < BH) {
         unn = un + gridDim.x;
       }
       if (un >= 0) fwd_dma_unit<NB>(lds + ((k + 1) & 1) * 2 * IMG, rs, un, ldq, N, H, dh, lane);
+      AST(sb + 1);
       wait_vm<0>();
+      AST(sb + 2);
+      asm volatile("" : "+v"(craw));
+      if (wq.q && claimer && un >= 0) unn = wq_claim_finish(craw, wq.base, BH);
       if (claimer) hand[k & 1] = unn;
     } else {
       const char* Ki = lds + (k & 1) * 2 * IMG;
       const char* Vi = Ki + IMG;
       bf16x8 qn[4];
-      if (un >= 0) fwd_load_q(qn, qkv, ldq, un, N, H, dh, q, hh);
+      if (un >= 0) load_q(qn, un);
       const int bh = u, b = u / H, h = u - b * H;
       const uint32_t row = drop_row(bh, N, q);
       float m = -INFINITY, l = 0.f;
@@ -372,7 +437,8 @@ __global__ __launch_bounds__(64 * (NB + 1)) void attn_fwd_pers(const bf16* __res
           }
           if (mask) {  // two independent writelane chains (lanes 0-15, 16-31)
             const uint32_t word = wl_keys8<0>(0u, bal) | wl_keys8<8>(0u, bal + 8);
-            if (lane < 32) mask[(((long)bh * NB + kb) * NB + w) * 32 + lane] = word;
+            __builtin_amdgcn_raw_buffer_store_b32(
+                word, rmk, mk_off, __builtin_amdgcn_readfirstlane((int)((((long)bh * NB + kb) * NB + w) * 128)), 0);
           }
         }
 #pragma unroll
@@ -382,16 +448,6 @@ __global__ __launch_bounds__(64 * (NB + 1)) void attn_fwd_pers(const bf16* __res
           for (int db = 0; db < 2; ++db) ot[db] = mfma32(vfr[s2][db], pf, ot[db]);
         }
       };
-      // Software-pipelined over key blocks: S^T of block kb+1 goes to the matrix pipe BEFORE the
-      // softmax / dropout VALU work of block kb, so the two overlap within the wave (the MFMA chain's
-      // latency was exposed at the head of every block); K fragments run two blocks ahead.
-      f32x16 st = {};
-#pragma unroll
-      for (int s = 0; s < 4; ++s) st = mfma32(kfr[s], qf[s], st);
-      if (NB > 1) {
-#pragma unroll
-        for (int s = 0; s < 4; ++s) kfr[s] = rd_row(Ki, 32 + (lane & 31), 2 * s + hh);
-      }
 #pragma unroll 1
       for (int kb = 0; kb < NB; ++kb) {
         bf16x8 vfr[2][2];
@@ -399,28 +455,38 @@ __global__ __launch_bounds__(64 * (NB + 1)) void attn_fwd_pers(const bf16* __res
         for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
           for (int db = 0; db < 2; ++db) vfr[s2][db] = rd_tr(Vi, kb * 32 + 16 * s2, db * 32, lane);
-        f32x16 sn = {};
+        f32x16 st = {};
+#pragma unroll
+        for (int s = 0; s < 4; ++s) st = mfma32(kfr[s], qf[s], st);
         if (kb + 1 < NB) {
 #pragma unroll
-          for (int s = 0; s < 4; ++s) sn = mfma32(kfr[s], qf[s], sn);
-          if (kb + 2 < NB) {
-#pragma unroll
-            for (int s = 0; s < 4; ++s) kfr[s] = rd_row(Ki, (kb + 2) * 32 + (lane & 31), 2 * s + hh);
-          }
+          for (int s = 0; s < 4; ++s) kfr[s] = rd_row(Ki, (kb + 1) * 32 + (lane & 31), 2 * s + hh);
         }
-        __builtin_amdgcn_sched_barrier(0);  // keep the next block's MFMAs ahead of this block's VALU
+        AST(sb + 1 + 2 * kb);
         block(kb, st, vfr);
-        st = sn;
+        AST(sb + 2 + 2 * kb);
       }
       l = xhalf_sum(l);
-      if (q < N) {
-        store_rows_q(out + ((long)b * N + q) * ldo + h * dh, ot[0], ot[1], dscale / l, hh, dh);
-        if (hh == 0) lse[(long)bh * N + q] = (m + log2f(l)) * LN2;
+      {
+        const float mul = dscale / l;
+        const int so = __builtin_amdgcn_readfirstlane((int)((((long)b * N) * ldo + h * dh) * 2));
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const f32x16& a = ot[i >> 2];
+          const int g4 = i & 3;
+          const bf16x4 v = {(bf16)(a[4 * g4] * mul), (bf16)(a[4 * g4 + 1] * mul), (bf16)(a[4 * g4 + 2] * mul),
+                            (bf16)(a[4 * g4 + 3] * mul)};
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), ro, o_off[i], so, 0);
+        }
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint((m + log2f(l)) * LN2), rl, lse_off,
+                                              __builtin_amdgcn_readfirstlane(bh * N * 4), 0);
       }
 #pragma unroll
       for (int s = 0; s < 4; ++s) qf[s] = qn[s];
+      AST(sb + 20);
     }
     bar_lds();  // the producer's DMA of unit un has landed (its wait_vm); every wave is done with unit u
+    AST(sb + 21);
     u = un;
     un = __builtin_amdgcn_readfirstlane(hand[k & 1]);
     if (u < 0) break;
@@ -463,8 +529,7 @@ FER_DEV bf16x8 rd_tr64(const char* img, int rbase, int lane) {
   const char* a2 = img + ds_off(R + 8 + q, c8);
   short4_t t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4_t*)a1);
   short4_t t2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4_t*)a2);
-  bf16x4 b1 = __builtin_bit_cast(bf16x4, t1), b2 = __builtin_bit_cast(bf16x4, t2);
-  return bf16x8{b1[0], b1[1], b1[2], b1[3], b2[0], b2[1], b2[2], b2[3]};
+  return cat8(t1, t2);
 }
 
 // Lane offsets of the LDS reads above, computed once per step instead of per read. The swizzles
@@ -488,8 +553,7 @@ FER_DEV TrB tr_base(int lane) {
 FER_DEV bf16x8 rd_trb(const char* img, const TrB& b, bool hi) {
   short4_t t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4_t*)(img + (hi ? (b.a1 ^ 64) : b.a1)));
   short4_t t2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4_t*)(img + (hi ? (b.a2 ^ 64) : b.a2)));
-  bf16x4 b1 = __builtin_bit_cast(bf16x4, t1), b2 = __builtin_bit_cast(bf16x4, t2);
-  return bf16x8{b1[0], b1[1], b1[2], b1[3], b2[0], b2[1], b2[2], b2[3]};
+  return cat8(t1, t2);
 }
 // == rd_row(img, R + (lane & 31), 2s + (lane >> 5)) for img + R * 128 passed as `img`
 FER_DEV int row_base(int lane) { return (lane & 31) * 128 + (((lane >> 5) ^ swz(lane & 31)) << 4); }
@@ -503,8 +567,7 @@ FER_DEV int2 tr64_base(int lane) {
 FER_DEV bf16x8 rd_tr64b(const char* img, int2 b) {
   short4_t t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4_t*)(img + b.x));
   short4_t t2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4_t*)(img + b.y));
-  bf16x4 b1 = __builtin_bit_cast(bf16x4, t1), b2 = __builtin_bit_cast(bf16x4, t2);
-  return bf16x8{b1[0], b1[1], b1[2], b1[3], b2[0], b2[1], b2[2], b2[3]};
+  return cat8(t1, t2);
 }
 
 // dQacc: [NB*32 queries][64 d] fp32, 16-byte chunk index XOR (row & 15)
@@ -762,7 +825,7 @@ __global__ __launch_bounds__(64 * NB) void attn_bwd_pers(
   constexpr int IMG = NB * 32 * 128;
   constexpr int PREP = NB >= 4 ? 3 : NB - 1;  // step whose dQ phase computes the next unit's Dq
   __shared__ __attribute__((aligned(1024))) char lds[pers_bwd_lds_bytes<NB>() + 16];
-  volatile int* hand = (volatile int*)(lds + pers_bwd_lds_bytes<NB>());  // unit hand-off (work queue)
+  lds_vint* hand = FER_LDS_INT(lds + pers_bwd_lds_bytes<NB>());  // unit hand-off (work queue)
   char* Kimg = lds + 4 * IMG;               // NB x [32 keys][64 d] images
   char* Sall = lds + 5 * IMG;               // NB x [32 keys][32 queries] bf16 dS tiles
   float* lsd = (float*)(Sall + NB * 2048);  // 2 x {L[NB*32] = -lse/scale, Dq[NB*32]}
@@ -778,8 +841,10 @@ __global__ __launch_bounds__(64 * NB) void attn_bwd_pers(
     char* Qi = lds + hb * 2 * IMG;
     img_dma_asm<NB>(Qi + IMG, rsrc4(dout), (long)b * N, lddo, h * dh, N, dh, w, lane);
     img_dma_asm<NB>(Qi, rsrc4(out), (long)b * N, ldo, h * dh, N, dh, w, lane);
-    const int r = w * 32 + lane;  // lanes 32..63 would land in the next wave's words: masked off
-    if (lane < 32) dma4_asm(lsd + hb * 2 * NB * 32 + w * 32, rsrc4(lse + (long)unit * N), r < N ? r * 4 : FER_OOB);
+    int ln = threadIdx.x & 63;  // recomputed here (laundered): a kept offset was spilled, and the scratch
+    asm volatile("" : "+v"(ln));  // reload's vmcnt(0) then waited for the previous unit's epilogue stores
+    const int r = w * 32 + ln;  // lanes 32..63 would land in the next wave's words: masked off
+    if (ln < 32) dma4_asm(lsd + hb * 2 * NB * 32 + w * 32, rsrc4(lse + (long)unit * N), r < N ? r * 4 : FER_OOB);
   };
   // after the DMA landed: L and Dq of this wave's rows, then its Q rows over the consumed O rows
   auto prep_finish = [&](int unit, int hb) {
@@ -803,14 +868,25 @@ __global__ __launch_bounds__(64 * NB) void attn_bwd_pers(
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // O rows read: Q may land on them
     img_dma_asm<NB>(Qi, rsrc4(qkv), (long)b * N, ldq, h * dh, N, dh, w, lane);
   };
-  auto load_frag = [&](bf16x8 (&vq)[4], int unit, int col0) {  // K (col0 = D) / V (2D) row fragments
-    const int b = unit / H, h = unit - b * H;
+  // K (col0 = D) / V (2D) row fragments and keep words by buffer loads, out-of-range lanes through the
+  // range check (FER_OOB): no per-lane branches, so the compiler's wait counts stay exact (with
+  // exec-masked loads it fell back to vmcnt(0) and the last step waited for the next unit's loads)
+  const __amdgpu_buffer_rsrc_t rq = make_rsrc(qkv);
+  const __amdgpu_buffer_rsrc_t rmk = make_rsrc(mask ? (const void*)mask : (const void*)qkv);
+  // per-lane byte offsets (computed once; the unit / column part goes into the scalar offset)
+  uint32_t kv_off[4];
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int d0 = 16 * s + 8 * hh;
-      vq[s] = (key < N && d0 < dh) ? *(const bf16x8*)(qkv + ((long)b * N + key) * ldq + col0 + h * dh + d0)
-                                   : bf16x8{};
-    }
+  for (int s = 0; s < 4; ++s) {
+    const int d0 = 16 * s + 8 * hh;
+    kv_off[s] = (key < N && d0 < dh) ? (uint32_t)(((long)key * ldq + d0) * 2) : FER_OOB;
+  }
+  const uint32_t mk_off = mask ? (uint32_t)((lane & 31) * 4) : FER_OOB;
+  auto load_frag = [&](bf16x8 (&vq)[4], int unit, int col0) {
+    const int b = unit / H, h = unit - b * H;
+    const int so = __builtin_amdgcn_readfirstlane((int)((((long)b * N) * ldq + col0 + h * dh) * 2));
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+      vq[s] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rq, kv_off[s], so, 0));
   };
   auto write_kimg = [&](const bf16x8 (&kq)[4]) {
 #pragma unroll
@@ -819,7 +895,8 @@ __global__ __launch_bounds__(64 * NB) void attn_bwd_pers(
   auto mask_word = [&](int unit, int i) -> uint32_t {  // keep word of (key block w, query block (w+i)%NB)
     int qb = w + i;
     if (qb >= NB) qb -= NB;
-    return mask ? mask[(((long)unit * NB + w) * NB + qb) * 32 + (lane & 31)] : 0xFFFFFFFFu;
+    const int so = __builtin_amdgcn_readfirstlane((int)((((long)unit * NB + w) * NB + qb) * 128));
+    return __builtin_amdgcn_raw_buffer_load_b32(rmk, mk_off, so, 0);  // (p = 0: 0, read as all-keep below)
   };
 
   // units: fixed stride, or the work queue `wq` (common.h): the first unit is blockIdx.x, the next
@@ -843,6 +920,8 @@ __global__ __launch_bounds__(64 * NB) void attn_bwd_pers(
   prep_finish(u, 0);
   write_kimg(kf);
   wait_vm<0>();
+  mwn = mask ? mwn : 0xFFFFFFFFu;
+  asm volatile("" : "+v"(mwn));  // resolved after the wait: the first step's use waits for nothing
   if (wq.q && threadIdx.x == 0) hand[2] = c0;
   bar_lds();
   if (wq.q) un = __builtin_amdgcn_readfirstlane(hand[2]);
@@ -861,15 +940,31 @@ __global__ __launch_bounds__(64 * NB) void attn_bwd_pers(
     f32x16 dq[2] = {f32x16{}, f32x16{}};  // dQ^T of query block w
     float cs = 0.f;                       // sum over this lane's query rows of dS[q][key]
     uint32_t mw0 = 0;                     // keep word of the next unit's first step
+    uint32_t claim_raw = 0;               // work queue: the claim issued in the last step
     // one step; the last is a separate instantiation (LAST) so that its extra work -- reloading
     // kf / vf with the next unit's fragments, the bias-gradient sums -- does not turn every
     // register it touches into a loop-carried copy
-    auto step = [&](int i, auto last_tag) {
+#ifdef FER_ATTN_STAMPS
+    const bool bst_on = blockIdx.x == 0 && (k == 2 || k == 3);
+    const int sb = (k - 2) * 64;
+#endif
+    BST(sb + 0);
+    // FIRST / LAST: the first step (its keep word resolved before the unit, so its use waits for no
+    // memory op -- in the loop it would wait for the previous unit's epilogue stores) and the last one
+    // (reloads kf / vf, bias-gradient sums) are separate instantiations
+    auto step = [&](int i, auto last_tag, auto first_tag) {
       constexpr bool LAST = decltype(last_tag)::value;
+      constexpr bool FIRST = decltype(first_tag)::value;
+      BST(sb + 1 + 7 * i);
       {
         int lane = threadIdx.x & 63;  // laundered per step: lane-derived LDS addresses are not
         asm volatile("" : "+v"(lane));  // hoisted out of the step loop (they would pin ~40 VGPRs)
         const int hh = lane >> 5;
+        // the keep word (loaded at the end of the previous step) is taken before any DMA of this step is
+        // issued: the DMA is inline asm, invisible to the compiler's wait counts, so its vmcnt(0) for
+        // the word would otherwise wait for the DMA as well
+        // bit acc_row(r, 0) = keep of query row r
+        const uint32_t mws = (FIRST ? mwn : (mask ? mwn : 0xFFFFFFFFu)) >> (4 * hh);
         if (i == 0 && has_next) prep_issue(un, cur ^ 1);
         int qb = w + i;
         if (qb >= NB) qb -= NB;
@@ -886,18 +981,28 @@ __global__ __launch_bounds__(64 * NB) void attn_bwd_pers(
           st[4 * g4 + 2] = l4[2];
           st[4 * g4 + 3] = l4[3];
         }
+        // LDS operands of each phase grouped ahead of its MFMAs (one exposed LDS latency per phase
+        // instead of one per MFMA)
+        bf16x8 qr[4], orr[4];
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
-          st = mfma32(rd_rowb(Qq, rb, s), kf[s], st);
-          dp = mfma32(rd_rowb(Oq, rb, s), vf[s], dp);
+          qr[s] = rd_rowb(Qq, rb, s);
+          orr[s] = rd_rowb(Oq, rb, s);
+        }
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          st = mfma32(qr[s], kf[s], st);
+          dp = mfma32(orr[s], vf[s], dp);
         }
         if (LAST && has_next) {  // kf / vf are dead from here on: the next unit's go straight in
           load_frag(kf, un, D);
           load_frag(vf, un, 2 * D);
           mw0 = mask_word(un, 0);
+          // the claim of the unit after next: its round trip overlaps the rest of this step (the
+          // result is read in the epilogue, after its wait)
+          if (wq.q && threadIdx.x == 0) claim_raw = wq_claim_issue(wq.q);
         }
-        const uint32_t mws = mwn >> (4 * hh);  // bit acc_row(r, 0) = keep of query row r
-        if (i + 1 < NB) mwn = mask_word(u, i + 1);
+        if (LAST) BST(sb + 54);
         f32x16 pd;
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4) {
@@ -919,13 +1024,21 @@ __global__ __launch_bounds__(64 * NB) void attn_bwd_pers(
         for (int g4 = 0; g4 < 4; ++g4)
           *(bf16x4*)(Si + ds_off(lane & 31, 2 * g4 + hh)) =
               bf16x4{(bf16)st[4 * g4], (bf16)st[4 * g4 + 1], (bf16)st[4 * g4 + 2], (bf16)st[4 * g4 + 3]};
+        bf16x8 ot_[2][2], qt_[2][2];
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+          for (int db = 0; db < 2; ++db) {
+            ot_[s2][db] = rd_trb(Oq + s2 * 2048, tb, db);
+            qt_[s2][db] = rd_trb(Qq + s2 * 2048, tb, db);
+          }
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
           const bf16x8 pf = pack8(pd, s2), df = pack8(st, s2);
 #pragma unroll
           for (int db = 0; db < 2; ++db) {
-            dv[db] = mfma32(pf, rd_trb(Oq + s2 * 2048, tb, db), dv[db]);
-            dk[db] = mfma32(df, rd_trb(Qq + s2 * 2048, tb, db), dk[db]);
+            dv[db] = mfma32(pf, ot_[s2][db], dv[db]);
+            dk[db] = mfma32(df, qt_[s2][db], dk[db]);
           }
         }
         if (LAST && cs_part) {  // this wave's keys: sum over all queries of dS
@@ -933,7 +1046,9 @@ __global__ __launch_bounds__(64 * NB) void attn_bwd_pers(
           if (hh == 0) csl[w * 32 + lane] = cs;
         }
       }
+      BST(sb + 2 + 7 * i);
       bar_lds();  // every dS tile of this step is in Sall
+      BST(sb + 3 + 7 * i);
       {
         int lane = threadIdx.x & 63;
         asm volatile("" : "+v"(lane));
@@ -944,13 +1059,19 @@ __global__ __launch_bounds__(64 * NB) void attn_bwd_pers(
         const char* Ko = Kimg + src * 4096;
         const TrB tb = tr_base(lane);
         const int2 t64 = tr64_base(lane);
+        bf16x8 sf[2], kt[2][2];
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
-          const bf16x8 sf = rd_tr64b(So + s2 * 1024, t64);
+          sf[s2] = rd_tr64b(So + s2 * 1024, t64);
 #pragma unroll
-          for (int db = 0; db < 2; ++db) dq[db] = mfma32(rd_trb(Ko + s2 * 2048, tb, db), sf, dq[db]);
+          for (int db = 0; db < 2; ++db) kt[s2][db] = rd_trb(Ko + s2 * 2048, tb, db);
         }
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+          for (int db = 0; db < 2; ++db) dq[db] = mfma32(kt[s2][db], sf[s2], dq[db]);
         if (i == PREP && has_next) prep_finish(un, cur ^ 1);
+        if (i + 1 < NB) mwn = mask_word(u, i + 1);  // after this step's DMA: its wait (next step) covers only this
         if (LAST && cs_part) {
           // colsum(dQ)[d] over this unit = sum_w K_w^T cs_w: B operand = cs of the wave's keys (k)
           // in every column (wave-private LDS read-back), A = K_w^T from its image.
@@ -980,32 +1101,61 @@ __global__ __launch_bounds__(64 * NB) void attn_bwd_pers(
           }
         }
       }
+      BST(sb + 4 + 7 * i);
       bar_lds();  // dS tiles and K images read: the next step may overwrite them
+      BST(sb + 5 + 7 * i);
         };
+    if constexpr (NB > 1) step(0, std::false_type{}, std::true_type{});
 #pragma unroll 1
-    for (int i = 0; i + 1 < NB; ++i) step(i, std::false_type{});
-    step(NB - 1, std::true_type{});
+    for (int i = 1; i + 1 < NB; ++i) step(i, std::false_type{}, std::false_type{});
+    step(NB - 1, std::true_type{}, std::bool_constant<NB == 1>{});
     // ---- epilogue of unit u (one barrier)
     if (has_next) {
-      // the claim's round trip overlaps this wait for the next unit's rows
-      if (wq.q && threadIdx.x == 0) unn = wq_claim(wq.q, wq.base, BH);
-      wait_vm<0>();  // this wave's DMA rows of the next unit, its K / V fragments, its mask word
+      wait_vm<0>();  // this wave's DMA rows of the next unit, its K / V fragments, its mask word, the claim
+      asm volatile("" : "+v"(claim_raw));  // read only after the wait above
+      if (wq.q && threadIdx.x == 0) unn = wq_claim_finish(claim_raw, wq.base, BH);
+      write_kimg(kf);  // the last step's dQ phase (barrier above) was the last reader of the K images
+      // the next unit's first keep word, consumed here (after the wait above, so the compiler's wait for
+      // it costs nothing) instead of in that unit's first step, where it would also wait for the stores
+      // this epilogue issues below
+      mw0 = mask ? mw0 : 0xFFFFFFFFu;
+      asm volatile("" : "+v"(mw0));
     }
+    BST(sb + 50);
     {
       const int b = u / H, h = u - b * H;
-      const int q = w * 32 + (lane & 31);
-      if (q < N) {  // dQ^T: lane = query, registers = 4 consecutive d per group
+      // dQ^T (lane = query, registers = 4 consecutive d per group) through a wave-private [32][64] bf16
+      // tile (16-byte chunk c of row r at c ^ (r & 7)), stored as whole 128-byte rows: the per-lane
+      // 8-byte stores at the row stride were store-issue bound (2k cycles per unit)
+      char* dqs = lds + cur * 2 * IMG + w * 8192;  // this unit's Q/dO half, wave-private
+      // every store below is a buffer store with out-of-range lanes at FER_OOB (dropped by the range
+      // check) instead of an exec-masked store: no divergent branches, so the compiler's vmcnt counts
+      // stay exact and later waits (the next unit's keep word) do not wait for these stores
+      const __amdgpu_buffer_rsrc_t rdq = make_rsrc(dqkv);
+      {
+        const int qr = lane & 31;
 #pragma unroll
         for (int db = 0; db < 2; ++db)
 #pragma unroll
           for (int g4 = 0; g4 < 4; ++g4) {
             const int d = db * 32 + 8 * g4 + 4 * hh;
-            if (d < dh)
-              *(bf16x4*)(dqkv + ((long)b * N + q) * lddq + h * dh + d) =
-                  bf16x4{(bf16)(dq[db][4 * g4] * scale), (bf16)(dq[db][4 * g4 + 1] * scale),
-                         (bf16)(dq[db][4 * g4 + 2] * scale), (bf16)(dq[db][4 * g4 + 3] * scale)};
+            *(bf16x4*)(dqs + qr * 128 + ((((d >> 3) ^ (qr & 7))) << 4) + (d & 4) * 2) =
+                bf16x4{(bf16)(dq[db][4 * g4] * scale), (bf16)(dq[db][4 * g4 + 1] * scale),
+                       (bf16)(dq[db][4 * g4 + 2] * scale), (bf16)(dq[db][4 * g4 + 3] * scale)};
           }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // wave-private: no barrier
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int t = i * 64 + lane, r = t >> 3, c = t & 7;
+          const int q = w * 32 + r;
+          const bf16x8 v = *(const bf16x8*)(dqs + r * 128 + ((c ^ (r & 7)) << 4));
+          const uint32_t off = (q < N && c * 8 < dh) ? (uint32_t)((((long)b * N + q) * lddq + h * dh + c * 8) * 2)
+                                                     : FER_OOB;
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rdq, off, 0, 0);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // read back before the dK / dV staging reuses it
       }
+      BST(sb + 51);
       if (cs_part) {
 #pragma unroll
         for (int db = 0; db < 2; ++db) {  // dK / dV column sums over this wave's valid key rows
@@ -1019,13 +1169,13 @@ __global__ __launch_bounds__(64 * NB) void attn_bwd_pers(
           tk = xhalf_sum(tk);
           tv = xhalf_sum(tv);
           const int d = db * 32 + (lane & 31);
-          float* o = cs_part + ((long)b * NB + w) * 3 * D + h * dh + d;
-          if (hh == 0 && d < dh) {
-            o[D] = tk * scale;
-            o[2 * D] = tv * dscale;
-          }
+          const uint32_t o = (hh == 0 && d < dh) ? (uint32_t)((((long)b * NB + w) * 3 * D + h * dh + d) * 4) : FER_OOB;
+          const __amdgpu_buffer_rsrc_t rcs = make_rsrc(cs_part);
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(tk * scale), rcs, o, D * 4, 0);
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(tv * dscale), rcs, o, 2 * D * 4, 0);
         }
       }
+      BST(sb + 52);
       bf16* stg = (bf16*)(lds + cur * 2 * IMG + w * 8192);  // [2][32][64], wave-private (this unit's Q/dO half)
 #pragma unroll
       for (int db = 0; db < 2; ++db)
@@ -1035,22 +1185,24 @@ __global__ __launch_bounds__(64 * NB) void attn_bwd_pers(
           stg[kr * 64 + d] = (bf16)(dk[db][r] * scale);
           stg[2048 + kr * 64 + d] = (bf16)(dv[db][r] * dscale);
         }
+      BST(sb + 53);
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const int t = i * 64 + lane;  // 512 chunks of 16 B: [2 mats][32 rows][8 chunks]
         const int mat = t >> 8, kr = (t >> 3) & 31, c = t & 7;
         const int gk = w * 32 + kr;
-        if (gk < N && c * 8 < dh)
-          *(bf16x8*)(dqkv + ((long)b * N + gk) * lddq + (1 + mat) * D + h * dh + c * 8) =
-              *(const bf16x8*)(stg + mat * 2048 + kr * 64 + c * 8);
+        const uint32_t off = (gk < N && c * 8 < dh)
+                                 ? (uint32_t)((((long)b * N + gk) * lddq + (1 + mat) * D + h * dh + c * 8) * 2)
+                                 : FER_OOB;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, *(const bf16x8*)(stg + mat * 2048 + kr * 64 + c * 8)),
+                                               rdq, off, 0, 0);
       }
     }
-    if (has_next) {
-      write_kimg(kf);  // the last step's dQ phase (barrier above) was the last reader of the K images
-      mwn = mw0;
-    }
+    if (has_next) mwn = mw0;
     if (threadIdx.x == 0) hand[cur] = unn;
+    BST(sb + 60);
     bar_lds();  // next unit: K / Q / dO images (each wave waited for its DMA), L / Dq; staging read
+    BST(sb + 61);
     u = un;
     un = __builtin_amdgcn_readfirstlane(hand[cur]);
     if (!has_next) break;
@@ -1483,6 +1635,15 @@ using namespace fer;
 
 int fer::set_step_ptr_attention(const uint64_t* p) { return set_step_ptr_here(p) == hipSuccess ? 0 : -1; }
 
+#ifdef FER_ATTN_STAMPS
+extern "C" int fer_debug_attn_stamps(unsigned long long* host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ast), sizeof(unsigned long long) * 9 * 64) == hipSuccess ? 0 : 1;
+}
+extern "C" int fer_debug_attn_bwd_stamps(unsigned long long* host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_bst), sizeof(unsigned long long) * 8 * 128) == hipSuccess ? 0 : 1;
+}
+#endif
+
 extern "C" int64_t fer_attention_ws(int dtype, int B, int N, int H) {
   // fp32 path: P and dS slabs, then the stand-alone colsum pass's partials; bf16: the fused
   // bias-gradient partials [B][3*H*64]
@@ -1623,7 +1784,8 @@ extern "C" int fer_attention_bwd(int dtype, const void* qkv, int64_t ld_qkv, con
   if (check_drop_range(drop_thresh, (long)B * H * N * (N + (N & 1)), "attention_bwd: dropout over >= 2^32 probabilities"))
     return -1;
   if (ld_qkv % 8 || ld_out % 8 || ld_dout % 8 || ld_dqkv % 8) return set_error("attention_bwd(bf16): misaligned ld");
-  if ((long)B * N * ld_qkv * 2 >= 0x7FFFFFF0L || (long)B * N * ld_dout * 2 >= 0x7FFFFFF0L)
+  if ((long)B * N * ld_qkv * 2 >= 0x7FFFFFF0L || (long)B * N * ld_dout * 2 >= 0x7FFFFFF0L ||
+      (long)B * N * ld_dqkv * 2 >= 0x7FFFFFF0L)
     return set_error("attention_bwd(bf16): operand exceeds 2 GiB (buffer-resource range)");
   const int nb = (N + 31) / 32;
   const float sl2 = scale * LOG2E;

@@ -25,6 +25,23 @@ typedef __attribute__((ext_vector_type(4))) float f32x4;
 typedef __attribute__((ext_vector_type(16))) float f32x16;
 typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
 typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
+// Global-typed 16-byte load (kernel-argument structs hold generic pointers: flat loads otherwise)
+FER_DEV f32x4 ldg_f32x4(const float* p) { return *(const __attribute__((address_space(1))) f32x4*)(const void*)p; }
+// A volatile int in LDS through an LDS-typed pointer: a plain `volatile int*` into a __shared__ array is a
+// generic pointer, compiled to flat_load / flat_store, which count in vmcnt AND lgkmcnt -- the compiler
+// then waits vmcnt(0) for the word, i.e. for every outstanding global store of the wave as well.
+typedef volatile __attribute__((address_space(3))) int lds_vint;
+typedef volatile __attribute__((address_space(3))) unsigned lds_vuint;
+#define FER_LDS_INT(p) ((lds_vint*)(__attribute__((address_space(3))) void*)(void*)(p))
+#define FER_LDS_UINT(p) ((lds_vuint*)(__attribute__((address_space(3))) void*)(void*)(p))
+// Two 4 x bf16 halves (e.g. two ds_read_b64_tr_b16 results) as one 8 x bf16 MFMA operand by
+// register concatenation: element-wise construction made hipcc repack every 16-bit element
+// (shift / and / or per element: ~8 VALU per operand in the attention and MN GEMM loops).
+FER_DEV bf16x8 cat8(short4_t a, short4_t b) {
+  const u32x2 x = __builtin_bit_cast(u32x2, a), y = __builtin_bit_cast(u32x2, b);
+  return __builtin_bit_cast(bf16x8, u32x4{x[0], x[1], y[0], y[1]});
+}
 
 enum { FER_ACT_NONE = 0, FER_ACT_GELU = 1, FER_ACT_RELU = 2, FER_ACT_MUL = 3 /* aux_act only: v *= aux */ };
 // act flag: `pre` receives the backward GATE act'(v) * keep * drop_scale instead of the
@@ -268,7 +285,9 @@ static __device__ const uint64_t* fer_step_ptr = nullptr;
 FER_DEV uint64_t step_seed(uint64_t seed) {
   const uint64_t* p = fer_step_ptr;
   if (!p) return seed;
-  uint64_t z = seed ^ (*p * 0x9E3779B97F4A7C15ull);
+  // global-typed load (a generic pointer compiles to a flat load: vmcnt AND lgkmcnt waits)
+  const uint64_t c = *(const __attribute__((address_space(1))) uint64_t*)(const void*)p;
+  uint64_t z = seed ^ (c * 0x9E3779B97F4A7C15ull);
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
   z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
   return z ^ (z >> 31);
@@ -400,6 +419,23 @@ FER_DEV int wq_claim(int* q, const uint32_t* base, int n) {
   const uint32_t t =
       (uint32_t)__hip_atomic_fetch_add(q + cls * FER_WQ_PAD, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) -
       base[cls];
+  const int nwg = ((int)gridDim.x - cls + 7) >> 3, items = (n - cls + 7) >> 3;
+  return (long)t < (long)items - nwg ? cls + 8 * (nwg + (int)t) : -1;
+}
+// The same claim in two halves: issue the atomic early, read its result only where it is needed (an
+// atomic with return counts in vmcnt: consuming it right away exposes the whole round trip).
+// The atomic is inline asm (a vector global_atomic_add with return, agent scope): the compiler's atomic
+// optimizer would otherwise wrap it in a wave reduction whose readfirstlane waits for the result at once.
+// The caller waits (s_waitcnt vmcnt) before reading the result, then passes it through an empty asm.
+FER_DEV uint32_t wq_claim_issue(int* q) {
+  uint32_t r;
+  int* p = q + (blockIdx.x & 7) * FER_WQ_PAD;
+  asm volatile("global_atomic_add %0, %1, %2, off sc0" : "=v"(r) : "v"(p), "v"(1) : "memory");
+  return r;
+}
+FER_DEV int wq_claim_finish(uint32_t raw, const uint32_t* base, int n) {
+  const int cls = blockIdx.x & 7;
+  const uint32_t t = raw - base[cls];
   const int nwg = ((int)gridDim.x - cls + 7) >> 3, items = (n - cls + 7) >> 3;
   return (long)t < (long)items - nwg ? cls + 8 * (nwg + (int)t) : -1;
 }

@@ -461,8 +461,7 @@ FER_DEV bf16x8 read_frag(const char* lds_tile, int i0, int kk, int lane) {
     const char* a2 = lds_tile + k2 * RB + ((c ^ mn_swz_t<MT>(k2)) << 4) + (p & 1) * 8;
     short4_t t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4_t*)a1);
     short4_t t2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4_t*)a2);
-    bf16x4 b1 = __builtin_bit_cast(bf16x4, t1), b2 = __builtin_bit_cast(bf16x4, t2);
-    return bf16x8{b1[0], b1[1], b1[2], b1[3], b2[0], b2[1], b2[2], b2[3]};
+    return cat8(t1, t2);
   }
 }
 
@@ -561,8 +560,8 @@ FER_DEV void tile_epilogue(const GemmArgs& g, const EpiArgs& e, AccT (&acc)[FN][
   const bool nok = n < g.N;  // N % 8 == 0 on this path (checked by the host)
   f32x4 b0 = f32x4{0.f, 0.f, 0.f, 0.f}, b1 = b0;
   if (e.bias && nok) {
-    b0 = *(const f32x4*)(e.bias + n);
-    b1 = *(const f32x4*)(e.bias + n + 4);
+    b0 = ldg_f32x4(e.bias + n);
+    b1 = ldg_f32x4(e.bias + n + 4);
   }
   const float ps = e.post_scale ? *e.post_scale : 1.f;
   const uint64_t seed = e.drop_thresh ? step_seed(e.seed) : 0;
@@ -1203,7 +1202,7 @@ FER_DEV unsigned long long stamp_now() {
 // prologue's operand DMA, and parks the id in that LDS word after the prologue's wait (which
 // retires the atomic together with the previous tile's epilogue stores and the first K-tile)
 template <bool AKC, bool BKC, int MT, int EK>
-FER_DEV void tile_8ph(const GemmArgs& g, const EpiArgs& e, int bid, char* smem, volatile int* claim_slot) {
+FER_DEV void tile_8ph(const GemmArgs& g, const EpiArgs& e, int bid, char* smem, lds_vint* claim_slot) {
   typedef typename Acc<MT>::T AccT;
   constexpr int UNIT = 16384, BUF = 4 * UNIT;  // A0 A1 B0 B1
   constexpr int FM = 128 / MT, FN = 64 / MT;   // MFMA blocks per wave (rows, cols)
@@ -1357,7 +1356,7 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmArgs g, EpiArgs e)
       bar_lds();  // every wave is done with the epilogue's LDS before the next tile's DMA
     }
   } else {
-    volatile int* slot = (volatile int*)(smem + 8 * 16384);
+    lds_vint* slot = FER_LDS_INT(smem + 8 * 16384);
     int bid = wq_first(ntiles), par = 0;
 #pragma unroll 1
     while (bid >= 0) {
@@ -1553,7 +1552,7 @@ __global__ __launch_bounds__(128 * WN, 1) void gemm_wgrad_group_kernel(WgGroup g
           __builtin_bit_cast(u32x4, acc[i][j]), rs, soff(ks, i, j), 0, 16 /* sc1: write-through */);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drained
     __syncthreads();
-    volatile unsigned* flag = (volatile unsigned*)(smem + NST * STAGE);
+    lds_vuint* flag = FER_LDS_UINT(smem + NST * STAGE);
     if (threadIdx.x == 0) {
       // the sc1 stores are write-through and drained: no release needed (MI355X_MICROARCH.md). The
       // last split also takes an agent-scope acquire before its sc1 loads: the sc1-only hand-off

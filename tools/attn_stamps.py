@@ -1,0 +1,80 @@
+"""Timeline of the persistent attention forward from the diagnostic stamp build (FER_ATTN_STAMPS):
+  FERVIT_LIB=fer-vit_amd/fervit/libfervit_st.so python tools/attn_stamps.py
+Workgroup 0, units 2 and 3: per wave, cycles from the unit's start to each stamp (consumers: per key
+block, before / after its softmax + P.V; producer: DMA issued, DMA landed; all: before / after the
+unit's barrier)."""
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "fer-vit_amd"))
+import torch  # noqa: E402
+
+from fervit import ops  # noqa: E402
+from fervit._lib import lib  # noqa: E402
+
+
+def main():
+    B, N, H, dh = 256, 197, 12, 64
+    D = H * dh
+    g = torch.Generator(device="cuda").manual_seed(0)
+    qkv = torch.randn(B * N, 3 * D, device="cuda", generator=g).to(torch.bfloat16)
+    out = torch.empty(B * N, D, device="cuda", dtype=torch.bfloat16)
+    for p in (0.1, 0.0):
+        lse = ops.attention_saved(qkv, B, N, H, dh, dropout=p)
+        for _ in range(3):
+            ops.attention_fwd(qkv, out, lse, B, N, H, dh, dropout=p, seed=5)
+        torch.cuda.synchronize()
+        buf = (ctypes.c_ulonglong * (9 * 64))()
+        assert lib().fer_debug_attn_stamps(buf) == 0
+        st = [list(buf[w * 64:(w + 1) * 64]) for w in range(9)]
+        print(f"p={p}")
+        for u in (0, 1):
+            base = min(st[w][u * 32] for w in range(8) if st[w][u * 32])
+            for w in range(8):
+                row = st[w][u * 32:u * 32 + 32]
+                if w == 7:
+                    pts = [("dma_issued", 1), ("dma_landed", 2), ("bar_out", 21)]
+                else:
+                    pts = [(f"kb{kb}", 2 + 2 * kb) for kb in range(7)] + [("end", 20), ("bar_out", 21)]
+                txt = " ".join(f"{n}={row[i] - base:6d}" for n, i in pts if row[i])
+                print(f"  unit{u} w{w} start={row[0] - base:6d} {txt}")
+
+
+
+
+def bwd():
+    B, N, H, dh = 256, 197, 12, 64
+    D = H * dh
+    g = torch.Generator(device="cuda").manual_seed(0)
+    qkv = torch.randn(B * N, 3 * D, device="cuda", generator=g).to(torch.bfloat16)
+    out = torch.empty(B * N, D, device="cuda", dtype=torch.bfloat16)
+    dout = torch.randn(B * N, D, device="cuda", generator=g).to(torch.bfloat16)
+    dqkv = torch.empty(B * N, 3 * D, device="cuda", dtype=torch.bfloat16)
+    lse = ops.attention_saved(qkv, B, N, H, dh, dropout=0.1)
+    ops.attention_fwd(qkv, out, lse, B, N, H, dh, dropout=0.1, seed=5)
+    for _ in range(3):
+        ops.attention_bwd(qkv, out, dout, lse, dqkv, B, N, H, dh, dropout=0.1, seed=5)
+    torch.cuda.synchronize()
+    buf = (ctypes.c_ulonglong * (8 * 128))()
+    assert lib().fer_debug_attn_bwd_stamps(buf) == 0
+    st = [list(buf[w * 128:(w + 1) * 128]) for w in range(8)]
+    print("bwd p=0.1 (per step: s=start d=dS written b1=after barrier 1 q=dQ done b2=after barrier 2)")
+    for u in (0, 1):
+        o = u * 64
+        base = min(st[w][o] for w in range(7) if st[w][o])
+        for w in range(7):
+            row = st[w][o:o + 64]
+            parts = []
+            for i in range(7):
+                s0, d, b1, q, b2 = (row[1 + 7 * i + j] - base for j in range(5))
+                parts.append(f"[{s0}|{d}|{b1}|{q}|{b2}]")
+            print(f"  unit{u} w{w} " + " ".join(parts) + f" last_loads={row[54] - base} epi: waited={row[50] - base} "
+                  f"dq={row[51] - base} cs={row[52] - base} stg={row[53] - base} end={row[60] - base} out={row[61] - base}")
+
+
+
+if __name__ == "__main__":
+    main()
+    bwd()

@@ -6,6 +6,10 @@ STEPS=${*:-tests bench prof}
 cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out && export TMPDIR=/tmp
 for s in $STEPS; do
   case $s in
+    ktests)  # attention / GEMM / LayerNorm kernel tests only
+      timeout -k 10 400 python -u -m pytest tests/test_gpu_kernels.py -m gpu -x -q -p no:cacheprovider --timeout 150 \
+        --timeout-method thread > gpurun_out/${TAG}_ktests.txt 2>&1 || { tail -30 gpurun_out/${TAG}_ktests.txt; exit 1; }
+      tail -2 gpurun_out/${TAG}_ktests.txt ;;
     tests)
       timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 150 \
         --timeout-method thread > gpurun_out/${TAG}_tests.txt 2>&1 || { tail -30 gpurun_out/${TAG}_tests.txt; exit 1; }
@@ -21,8 +25,12 @@ for s in $STEPS; do
         (cd tools && FERVIT_LIB=$GRAFT_REPO_ROOT/fer-vit_amd/fervit/$lib timeout -k 10 200 python -u ${s}_bench.py 2>&1 \
           | grep -v amdgpu.ids | sed "s/^/[$lib] /") | tee -a gpurun_out/${TAG}_${s}_ab.txt || exit 1
       done; done ;;
+    astamps)
+      FERVIT_LIB=$GRAFT_REPO_ROOT/fer-vit_amd/fervit/libfervit_st.so timeout -k 10 120 python -u tools/attn_stamps.py \
+        > gpurun_out/${TAG}_attn_stamps.txt 2>&1 || { tail -20 gpurun_out/${TAG}_attn_stamps.txt; exit 1; }
+      cat gpurun_out/${TAG}_attn_stamps.txt | grep -v amdgpu.ids ;;
     prof)
-      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_prof -o run -- \
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof -o run -- \
         python3 bench.py --steps 10 --warmup 5 --no-cpu-baseline --no-traffic > gpurun_out/${TAG}_prof.json 2>&1 \
         || { tail -20 gpurun_out/${TAG}_prof.json; exit 1; }
       f=$(find gpurun_out/${TAG}_prof -name "*kernel_stats.csv" | head -1)
