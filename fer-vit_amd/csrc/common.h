@@ -217,42 +217,44 @@ FER_DEV void gelu_and_grad8(f32x2 (&x)[4], f32x2 (&grad)[4]) {
 // x^2 * (-log2(e)/2): same formulas, roundings in a different order.
 // hs = {s/2, s/2}, ps = {s/sqrt(2 pi), s/sqrt(2 pi)} (computed once by the caller, outside any
 // divergent branch).
-FER_DEV void gelu_and_grad8s(f32x2 (&x)[4], f32x2 (&grad)[4], f32x2 hs, f32x2 ps) {
-  f32x2 e[4], z[4], t[4], y[4];
+template <int P>
+FER_DEV void gelu_and_grad_ps(f32x2 (&x)[P], f32x2 (&grad)[P], f32x2 hs, f32x2 ps) {
+  f32x2 e[P], z[P], t[P], y[P];
   const f32x2 kh = kpk(-0.72134752044448170f);  // -log2(e) / 2
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < P; ++i) {
     const f32x2 h = x[i] * x[i] * kh;
     e[i] = f32x2{__builtin_amdgcn_exp2f(h[0]), __builtin_amdgcn_exp2f(h[1])};
   }
 #pragma unroll
-  for (int i = 0; i < 4; ++i) z[i] = x[i] * 0.70710678118654752f;
+  for (int i = 0; i < P; ++i) z[i] = x[i] * 0.70710678118654752f;
   const f32x2 ka = kpk(0.3275911f);
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < P; ++i) {
     const f32x2 d = __builtin_elementwise_fma(ka, __builtin_elementwise_abs(z[i]), f32x2(1.0f));
     t[i] = f32x2{__builtin_amdgcn_rcpf(d[0]), __builtin_amdgcn_rcpf(d[1])};
   }
   const f32x2 k0 = kpk(1.061405429f), k1 = kpk(-1.453152027f);
 #pragma unroll
-  for (int i = 0; i < 4; ++i) y[i] = __builtin_elementwise_fma(k0, t[i], k1);
+  for (int i = 0; i < P; ++i) y[i] = __builtin_elementwise_fma(k0, t[i], k1);
   const f32x2 k2 = kpk(1.421413741f);
 #pragma unroll
-  for (int i = 0; i < 4; ++i) y[i] = __builtin_elementwise_fma(y[i], t[i], k2);
+  for (int i = 0; i < P; ++i) y[i] = __builtin_elementwise_fma(y[i], t[i], k2);
   const f32x2 k3 = kpk(-0.284496736f);
 #pragma unroll
-  for (int i = 0; i < 4; ++i) y[i] = __builtin_elementwise_fma(y[i], t[i], k3);
+  for (int i = 0; i < P; ++i) y[i] = __builtin_elementwise_fma(y[i], t[i], k3);
   const f32x2 k4 = kpk(0.254829592f);
 #pragma unroll
-  for (int i = 0; i < 4; ++i) y[i] = __builtin_elementwise_fma(y[i], t[i], k4);
+  for (int i = 0; i < P; ++i) y[i] = __builtin_elementwise_fma(y[i], t[i], k4);
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < P; ++i) {
     const f32x2 r = 1.0f - y[i] * t[i] * e[i];
     const f32x2 cdf = __builtin_elementwise_fma(hs, __builtin_elementwise_copysign(r, z[i]), hs);  // s * Phi(x)
     grad[i] = __builtin_elementwise_fma(x[i] * ps, e[i], cdf);
     x[i] = x[i] * cdf;
   }
 }
+FER_DEV void gelu_and_grad8s(f32x2 (&x)[4], f32x2 (&grad)[4], f32x2 hs, f32x2 ps) { gelu_and_grad_ps<4>(x, grad, hs, ps); }
 FER_DEV float act_fwd(int act, float x) {
   return act == FER_ACT_GELU ? gelu_erf(x) : (act == FER_ACT_RELU ? fmaxf(x, 0.f) : x);
 }

@@ -213,9 +213,12 @@ FER_DEV void epi8_t(const EpiArgs& e, long m, long n, f32x4& v0, f32x4& v1, f32x
 // the dropout scale folded into constants: GATE takes it in the GELU constants (gelu_and_grad8s),
 // RES as acc * (alpha*s) + b*s (ab = alpha*s, b0 / b1 pre-scaled by the caller), so a dropped
 // element costs a select only.
+// Outputs go out as buffer stores at byte offsets ocb / opb (FER_OOB for a row out of range: the
+// store is dropped without a branch, so the compiler's wait counts around it stay exact).
 template <int S0>
-FER_DEV void epi8_k(const EpiArgs& e, long oc, long op, uint32_t di, f32x4& v0, f32x4& v1, f32x4 b0, f32x4 b1,
-                    bf16x8 x, uint64_t seed, float ab, f32x2 ghs, f32x2 gps, float dsr) {
+FER_DEV void epi8_k(const EpiArgs& e, uint32_t ocb, uint32_t opb, uint32_t di, f32x4& v0, f32x4& v1, f32x4 b0,
+                    f32x4 b1, bf16x8 x, uint64_t seed, float ab, f32x2 ghs, f32x2 gps, float dsr,
+                    const __amdgpu_buffer_rsrc_t& rc, const __amdgpu_buffer_rsrc_t& rp) {
   constexpr int S = epi_base(S0);
   static_assert(S != EPI_GEN, "generic epilogue goes through epi8_t");
   v0 = v0 * ab + b0;
@@ -232,7 +235,7 @@ FER_DEV void epi8_k(const EpiArgs& e, long oc, long op, uint32_t di, f32x4& v0, 
       v0[r] = k0 ? fmaxf(v0[r], 0.f) : 0.f;
       v1[r] = k1 ? fmaxf(v1[r], 0.f) : 0.f;
     }
-    *(bf16x8*)((bf16*)e.pre + op) = pack8(g0, g1);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, pack8(g0, g1)), rp, opb, 0, 0);
   }
   if constexpr (S == EPI_GATE) {
     f32x4 g0, g1;
@@ -251,7 +254,7 @@ FER_DEV void epi8_k(const EpiArgs& e, long oc, long op, uint32_t di, f32x4& v0, 
         g1[r] = kp[4 + r] ? g1[r] : 0.f;
       }
     }
-    *(bf16x8*)((bf16*)e.pre + op) = pack8(g0, g1);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, pack8(g0, g1)), rp, opb, 0, 0);
   }
   if constexpr (S == EPI_RES) {
     if (e.drop_thresh) {
@@ -270,12 +273,20 @@ FER_DEV void epi8_k(const EpiArgs& e, long oc, long op, uint32_t di, f32x4& v0, 
     v0 *= lo4(x);
     v1 *= hi4(x);
   }
-  *(bf16x8*)((bf16*)e.c + oc) = pack8(v0, v1);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, pack8(v0, v1)), rc, ocb, 0, 0);
 }
 
 // kind for a launch (EPI_GEN unless every flag matches one of the fixed kinds)
-static inline int epi_kind(const EpiArgs& e) {
+// The fixed kinds address c / pre / res / aux through 32-bit buffer offsets (out-of-range rows at
+// FER_OOB): each operand must span less than 2 GiB, else the generic epilogue runs.
+static inline bool epi_span_ok(const void* p, long ld, long M, long N) {
+  return !p || ((M - 1) * ld + N) * 2 < 0x7FFFFFF0L;
+}
+static inline int epi_kind(const EpiArgs& e, long M, long N) {
   if (e.c_f32 || e.accumulate || e.post_scale) return EPI_GEN;
+  if (!epi_span_ok(e.c, e.ldc, M, N) || !epi_span_ok(e.pre, e.ldp, M, N) || !epi_span_ok(e.res, e.ldr, M, N) ||
+      !epi_span_ok(e.aux, e.ldx, M, N))
+    return EPI_GEN;
   const int act = e.act & 15;
   const bool gate = (e.act & FER_PRE_GATE) && e.pre;
   if (gate) {
@@ -577,7 +588,7 @@ FER_DEV void tile_epilogue(const GemmArgs& g, const EpiArgs& e, AccT (&acc)[FN][
   const f32x2 ghs = f32x2(0.5f * dsc), gps = f32x2(0.39894228040143268f * dsc);  // GATE: gelu_and_grad8s
   const void* xs = e.res ? e.res : e.aux;  // the row operand brought in by DMA
   const long ldxs = e.res ? e.ldr : e.ldx;
-  const __amdgpu_buffer_rsrc_t rx = make_rsrc(xs);
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(xs), rc = make_rsrc(e.c), rp = make_rsrc(e.pre ? e.pre : e.c);
   // this lane's DMA source for piece k of chunk 0 (rows advance by EROWS per chunk)
   const int xrow = lane / LPR, xcol = (lane % LPR) * 8;
   const bool xcol_ok = n0 + xcol + 8 <= g.N;
@@ -639,9 +650,16 @@ FER_DEV void tile_epilogue(const GemmArgs& g, const EpiArgs& e, AccT (&acc)[FN][
       const long m = m0 + h * EROWS + r;
       f32x4 v0 = *(const f32x4*)(stg + swz(r, tc)), v1 = *(const f32x4*)(stg + swz(r, tc + 4));
       const bf16x8 x = xs ? *(const bf16x8*)(xh + (r * BN + tc) * 2) : bf16x8{};
-      if (nok && m < g.M) {
-        if constexpr (KIND) epi8_k<EK>(e, oc, op, di, v0, v1, b0, b1, x, seed, ab, ghs, gps, dsc);
-        else epi8_t<EK>(e, m, n, v0, v1, b0, b1, x, ps, seed);
+      const bool ok = nok && m < g.M;
+      if constexpr (KIND) {
+        epi8_k<EK>(e, ok ? (uint32_t)(oc * 2) : FER_OOB, ok ? (uint32_t)(op * 2) : FER_OOB, di, v0, v1, b0, b1, x,
+                   seed, ab, ghs, gps, dsc, rc, rp);
+        if constexpr (CS) {
+          cs0 += ok ? v0 : f32x4{0.f, 0.f, 0.f, 0.f};
+          cs1 += ok ? v1 : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+      } else if (ok) {
+        epi8_t<EK>(e, m, n, v0, v1, b0, b1, x, ps, seed);
         if constexpr (CS) {
           cs0 += v0;
           cs1 += v1;
@@ -657,17 +675,20 @@ FER_DEV void tile_epilogue(const GemmArgs& g, const EpiArgs& e, AccT (&acc)[FN][
     // staging (round 0's at entry, round 1's once round 0's accumulators are in LDS), so they fly
     // during the staging and the other round; loads issued before the stores retire first (vmcnt)
     const bf16* xg = (const bf16*)xs;
+    // branch-free: out-of-range rows load zeros / drop their stores through FER_OOB offsets, so the
+    // compiler counts the round's loads exactly instead of draining every store before their use
+    const uint32_t ldxb = (uint32_t)ldxs * 2, ldcb = (uint32_t)e.ldc * 2;
     auto load_x = [&](int p, bf16x8 (&xr)[2 * IT]) {
 #pragma unroll
       for (int k = 0; k < 2 * IT; ++k) {
         const long m = m0 + ((k / IT) * EPC + p) * EROWS + tr + (k % IT) * RPI;
-        xr[k] = (nok && m < g.M) ? *(const bf16x8*)(xg + m * ldxs + n) : bf16x8{};
+        const uint32_t off = (nok && m < g.M) ? (uint32_t)m * ldxb + (uint32_t)n * 2 : FER_OOB;
+        xr[k] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rx, off, 0, 0));
       }
     };
     auto finish_x = [&](int h, const char* stg, const bf16x8* xr) {
       f32x4 v0 = *(const f32x4*)(stg + swz(tr, tc)), v1 = *(const f32x4*)(stg + swz(tr, tc + 4));
       const long mr = m0 + h * EROWS + tr;
-      const long oc0 = mr * e.ldc + n;
       const uint32_t di0 = (uint32_t)mr * (uint32_t)e.drop_ld + (uint32_t)n;
 #pragma unroll
       for (int it = 0; it < IT; ++it) {
@@ -678,13 +699,13 @@ FER_DEV void tile_epilogue(const GemmArgs& g, const EpiArgs& e, AccT (&acc)[FN][
           n0 = *(const f32x4*)(stg + swz(r + RPI, tc));
           n1 = *(const f32x4*)(stg + swz(r + RPI, tc + 4));
         }
-        if (nok && m < g.M) {
-          epi8_k<EK>(e, oc0 + (long)it * RPI * e.ldc, 0, di0 + (uint32_t)(it * RPI) * (uint32_t)e.drop_ld, v0, v1,
-                     b0, b1, xr[it], seed, ab, ghs, gps, dsc);
-          if constexpr (CS) {
-            cs0 += v0;
-            cs1 += v1;
-          }
+        const bool ok = nok && m < g.M;
+        epi8_k<EK>(e, ok ? (uint32_t)m * ldcb + (uint32_t)n * 2 : FER_OOB, FER_OOB,
+                   di0 + (uint32_t)(it * RPI) * (uint32_t)e.drop_ld, v0, v1, b0, b1, xr[it], seed, ab, ghs, gps, dsc,
+                   rc, rp);
+        if constexpr (CS) {
+          cs0 += ok ? v0 : f32x4{0.f, 0.f, 0.f, 0.f};
+          cs1 += ok ? v1 : f32x4{0.f, 0.f, 0.f, 0.f};
         }
         v0 = n0;
         v1 = n1;
@@ -702,8 +723,11 @@ FER_DEV void tile_epilogue(const GemmArgs& g, const EpiArgs& e, AccT (&acc)[FN][
                 f32x4{acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]};
           }
     };
-    bf16x8 xr[2 * IT];
+    // both rounds' rows are issued up front (round 1's before round 0's stores: vmcnt retires in
+    // issue order, so a load issued after the stores would wait for them)
+    bf16x8 xr[2 * IT], xr1[2 * IT];
     load_x(0, xr);
+    load_x(1, xr1);
     bar_lds();
     put(std::integral_constant<int, 0>{});
     bar_lds();
@@ -712,14 +736,13 @@ FER_DEV void tile_epilogue(const GemmArgs& g, const EpiArgs& e, AccT (&acc)[FN][
     EP_STAMP(2);
     finish_x(EPC, stg + EROWS * SROW, xr + IT);
     EP_STAMP(3);
-    load_x(1, xr);
     bar_lds();
     put(std::integral_constant<int, 1>{});
     bar_lds();
     EP_STAMP(5);
-    finish_x(1, stg, xr);
+    finish_x(1, stg, xr1);
     EP_STAMP(6);
-    finish_x(EPC + 1, stg + EROWS * SROW, xr + IT);
+    finish_x(EPC + 1, stg + EROWS * SROW, xr1 + IT);
     EP_STAMP(7);
     EP_STAMP(4);
     EP_STAMP(8);
@@ -1095,7 +1118,7 @@ static int launch_pp(GemmArgs g, const EpiArgs& e, hipStream_t st) {
   g.tiles_n = (g.N + 127) / 128;
   const dim3 grid(g.tiles_m * g.tiles_n, g.splits);
   // fixed-flag epilogue kinds as in the 8-phase kernel (K-contiguous operands, no split-K)
-  const int ek = (AKC && BKC && !g.partial) ? epi_kind(e) : EPI_GEN;
+  const int ek = (AKC && BKC && !g.partial) ? epi_kind(e, g.M, g.N) : EPI_GEN;
 #define FER_PPK(K) hipLaunchKernelGGL((gemm_pp_kernel<AKC, BKC, K>), grid, dim3(256), 0, st, g, e)
   if constexpr (AKC && BKC) {
     switch (ek) {
@@ -1197,6 +1220,114 @@ FER_DEV unsigned long long stamp_now() {
 #else
 #define FER_STAMP(i) do {} while (0)
 #endif
+
+// Wave-private epilogue of the 8-phase kernel (fixed kinds, MFMA 16x16). Each wave stages its own
+// 128 x 64 accumulator region through its own 16 KB of LDS (the main loop's operand buffers) in
+// 32-row chunks of fp32, XOR-swizzled by row, and reads it back row-contiguous: lane = (row
+// lane >> 3 of an 8-row pass, 8 columns 8 (lane & 7)), so the kind's arithmetic (epi8_k), the
+// row operand's loads (RES / MUL, 16 B per lane, one chunk ahead) and the output stores (16 B per
+// lane, whole 128-byte rows per 8 lanes) are row-contiguous. No workgroup barrier between chunks:
+// the workgroup-wide staging (all waves through two shared areas, four stage / finish rounds with
+// barriers) spent 28-34 k cycles per GELU-gate tile mostly waiting at those barriers for the slower
+// wave-row half. (Storing straight from the accumulator layout -- 8 bytes per lane, 16 rows per
+// instruction -- measured 10-25 % slower kernels: profiles/r04k_gemm_ab.txt.)
+// MUL's fused column sums (cs_part): per lane over its rows, over the 8 row lanes of a column group,
+// then the two wave-row halves through LDS.
+template <int EK>
+FER_DEV void tile_epilogue_wp(const GemmArgs& g, const EpiArgs& e, f32x4 (&acc)[4][8], char* smem, int m0, int n0,
+                              int wr, int wc, int lane) {
+  constexpr int S = epi_base(EK);
+  constexpr bool X = S == EPI_RES || S == EPI_MUL;
+  constexpr bool CS = S == EPI_MUL;
+  const int wave = wr * 4 + wc;
+  char* const ws = smem + wave * 16384;  // two 8 KB chunk buffers
+  // staging write: block (i, j) of the chunk -> local row 16 (j & 1) + (lane & 15), column 16 i + 4 (lane >> 4)
+  auto swz = [](int row, int c16) { return row * 256 + ((c16 ^ (row & 15)) << 4); };
+  const int prow = lane >> 3, pc = 8 * (lane & 7);  // read-back: row of the pass, first column
+  const int n = n0 + wc * 64 + pc;
+  const bool nok = n < g.N;  // N % 8 == 0 on this path (checked by the host)
+  const float dsc = e.drop_thresh ? e.drop_scale : 1.f;
+  const float ab = (S == EPI_RES || EK == EPI_GATER) ? e.alpha * dsc : e.alpha;
+  const f32x2 ghs = f32x2(0.5f * dsc), gps = f32x2(0.39894228040143268f * dsc);
+  const uint64_t seed = e.drop_thresh ? step_seed(e.seed) : 0;
+  f32x4 b0 = f32x4{0.f, 0.f, 0.f, 0.f}, b1 = b0;
+  if (e.bias && nok) {
+    b0 = ldg_f32x4(e.bias + n);
+    b1 = ldg_f32x4(e.bias + n + 4);
+  }
+  if (S == EPI_RES || EK == EPI_GATER) {
+    b0 *= dsc;
+    b1 *= dsc;
+  }
+  const __amdgpu_buffer_rsrc_t rc = make_rsrc(e.c), rp = make_rsrc(e.pre ? e.pre : e.c);
+  const void* xs = e.res ? e.res : e.aux;
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(X && xs ? xs : e.c);
+  const uint32_t ldcb = (uint32_t)e.ldc * 2, ldpb = (uint32_t)e.ldp * 2;
+  const uint32_t ldxb = X ? (uint32_t)(e.res ? e.ldr : e.ldx) * 2 : 0u;
+  const int rw0 = m0 + wr * 128 + prow;  // this lane's row in pass 0 of chunk 0
+  auto load_x = [&](int c, bf16x8 (&xc)[4]) {
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int row = rw0 + c * 32 + p * 8;
+      const uint32_t off = (nok && row < g.M) ? (uint32_t)row * ldxb + (uint32_t)n * 2 : FER_OOB;
+      xc[p] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rx, off, 0, 0));
+    }
+  };
+  f32x4 cs0 = f32x4{0.f, 0.f, 0.f, 0.f}, cs1 = cs0;
+  bf16x8 xr[2][4];
+  if constexpr (X) load_x(0, xr[0]);
+  bar_lds();  // every wave is done with the main loop's operand buffers
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    char* const buf = ws + (c & 1) * 8192;
+    if constexpr (X) {
+      if (c + 1 < 4) load_x(c + 1, xr[(c + 1) & 1]);
+    }
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        *(f32x4*)(buf + swz(16 * jj + (lane & 15), 4 * i + (lane >> 4))) = acc[i][2 * c + jj];
+    // (a wave's own LDS writes are complete for its later reads: in-order LDS, no barrier)
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int lrow = p * 8 + prow;
+      f32x4 v0 = *(const f32x4*)(buf + swz(lrow, pc >> 2)), v1 = *(const f32x4*)(buf + swz(lrow, (pc >> 2) + 1));
+      const int row = rw0 + c * 32 + p * 8;
+      const bool ok = nok && row < g.M;
+      const uint32_t di = (uint32_t)row * (uint32_t)e.drop_ld + (uint32_t)n;
+      epi8_k<EK>(e, ok ? (uint32_t)row * ldcb + (uint32_t)n * 2 : FER_OOB,
+                 ok ? (uint32_t)row * ldpb + (uint32_t)n * 2 : FER_OOB, di, v0, v1, b0, b1,
+                 X ? xr[c & 1][p] : bf16x8{}, seed, ab, ghs, gps, dsc, rc, rp);
+      if constexpr (CS) {
+        cs0 += ok ? v0 : f32x4{0.f, 0.f, 0.f, 0.f};
+        cs1 += ok ? v1 : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+  }
+  if constexpr (CS) {
+    if (g.cs_part) {
+      // over the 8 row lanes of the column group (lanes 8 apart), fixed order
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+#pragma unroll
+        for (int d = 8; d < 64; d <<= 1) {
+          cs0[r] += __shfl_xor(cs0[r], d);
+          cs1[r] += __shfl_xor(cs1[r], d);
+        }
+      }
+      float* red = (float*)smem;  // [2 wave-row halves][256 columns]
+      bar_lds();                  // every wave is done with its staging
+      if (prow == 0) {
+        *(f32x4*)(red + wr * 256 + wc * 64 + pc) = cs0;
+        *(f32x4*)(red + wr * 256 + wc * 64 + pc + 4) = cs1;
+      }
+      bar_lds();
+      const int t = threadIdx.x;
+      if (t < 256 && n0 + t < g.N) g.cs_part[(long)(m0 / 256) * g.N + n0 + t] = red[t] + red[256 + t];
+    }
+  }
+}
 
 // claim_slot (work-queue mode): thread 0 claims a tile at the start of this one, before the
 // prologue's operand DMA, and parks the id in that LDS word after the prologue's wait (which
@@ -1327,7 +1458,10 @@ FER_DEV void tile_8ph(const GemmArgs& g, const EpiArgs& e, int bid, char* smem, 
   if (nk > 0 && !wr) __builtin_amdgcn_s_barrier();  // waves 0-3 catch up with the stagger
   FER_STAMP(2);
   static_assert(64 * (256 + 4) * 4 <= 2 * BUF, "epilogue staging (2 chunks per half) must fit");
-  tile_epilogue<256, 256, 2, 4, MT, 2, 2 * BUF, EK>(g, e, acc, smem, m0, n0, ks, wr, wc, lane);
+  if constexpr (EK != EPI_GEN && MT == 16)
+    tile_epilogue_wp<EK>(g, e, acc, smem, m0, n0, wr, wc, lane);
+  else
+    tile_epilogue<256, 256, 2, 4, MT, 2, 2 * BUF, EK>(g, e, acc, smem, m0, n0, ks, wr, wc, lane);
   FER_STAMP(3);
 #ifdef FER_GEMM_STAMPS
   if (st_on) {
@@ -1604,7 +1738,7 @@ static int launch_bf16(GemmArgs g, const EpiArgs& e, hipStream_t st) {
   // the 128^2 K-contiguous MT16 kernel (the small-grid configs: w+ latents, 48 px) also gets the
   // fixed-flag epilogues (row operands through its LDS-DMA staging: the LDS-DMA kinds)
   if constexpr (BM == 128 && (BN == 128 || BN == 64) && AKC && BKC && MT == 16) {
-    int ek = g.partial ? EPI_GEN : epi_kind(e);
+    int ek = g.partial ? EPI_GEN : epi_kind(e, g.M, g.N);
     if (ek == EPI_RES2) ek = EPI_RES;
     if (ek == EPI_MUL2) ek = EPI_MUL;
     switch (ek) {
@@ -1654,7 +1788,7 @@ static int launch_8ph(GemmArgs g, const EpiArgs& e, hipStream_t st) {
   }
   dim3 grid(gx, g.splits);
   // fixed-flag epilogues for the K-contiguous MT16 kernel (the forward and transposed-shadow dgrad path)
-  const int ek = (AKC && BKC && MT == 16 && !g.partial) ? epi_kind(e) : EPI_GEN;
+  const int ek = (AKC && BKC && MT == 16 && !g.partial) ? epi_kind(e, g.M, g.N) : EPI_GEN;
 #define FER_8PH(DY, K) hipLaunchKernelGGL((gemm_8ph_kernel<AKC, BKC, MT, DY, K>), grid, dim3(512), 0, st, g, e)
 #define FER_8PH_K(DY)                                  \
   if constexpr (AKC && BKC && MT == 16) {              \

@@ -40,6 +40,24 @@ def main():
                     pts = [(f"kb{kb}", 2 + 2 * kb) for kb in range(7)] + [("end", 20), ("bar_out", 21)]
                 txt = " ".join(f"{n}={row[i] - base:6d}" for n, i in pts if row[i])
                 print(f"  unit{u} w{w} start={row[0] - base:6d} {txt}")
+        wg_stats()
+
+
+def wg_stats():
+    """Per-workgroup units, core cycles and wall time (s_memrealtime, 100 MHz) of the last forward."""
+    buf = (ctypes.c_ulonglong * (1024 * 5))()
+    if not hasattr(lib(), "fer_debug_attn_wg_stats") or lib().fer_debug_attn_wg_stats(buf) != 0:
+        return
+    rows = [buf[i * 5:(i + 1) * 5] for i in range(1024)]
+    rows = [r for r in rows if r[0]]
+    units = [r[0] for r in rows]
+    cyc = [r[2] - r[1] for r in rows]
+    wall = [(r[4] - r[3]) / 100.0 for r in rows]  # us
+    t0 = min(r[3] for r in rows)
+    last = max(r[4] for r in rows)
+    print(f"  WGs {len(rows)}  units/WG min {min(units)} max {max(units)}  kernel span {(last - t0) / 100.0:.1f} us  "
+          f"WG wall min {min(wall):.1f} max {max(wall):.1f} us  clock {sum(cyc) / sum(wall) / 1e3:.2f} GHz  "
+          f"cycles/unit {sum(cyc) / sum(units):.0f}")
 
 
 

@@ -20,7 +20,7 @@ for s in $STEPS; do
       cut -c1-400 gpurun_out/${TAG}_bench.json ;;
     attn|gemm|ln)
       # A/B microbench: the in-tree library and fer-vit_amd/fervit/libfervit_base.so (if present), interleaved
-      for rep in 1 2; do for lib in libfervit.so libfervit_base.so; do
+      for rep in 1 2; do for lib in ${ABLIBS:-libfervit.so libfervit_base.so}; do
         [ -f fer-vit_amd/fervit/$lib ] || continue
         (cd tools && FERVIT_LIB=$GRAFT_REPO_ROOT/fer-vit_amd/fervit/$lib timeout -k 10 200 python -u ${s}_bench.py 2>&1 \
           | grep -v amdgpu.ids | sed "s/^/[$lib] /") | tee -a gpurun_out/${TAG}_${s}_ab.txt || exit 1
@@ -29,6 +29,11 @@ for s in $STEPS; do
       FERVIT_LIB=$GRAFT_REPO_ROOT/fer-vit_amd/fervit/libfervit_st.so timeout -k 10 120 python -u tools/attn_stamps.py \
         > gpurun_out/${TAG}_attn_stamps.txt 2>&1 || { tail -20 gpurun_out/${TAG}_attn_stamps.txt; exit 1; }
       cat gpurun_out/${TAG}_attn_stamps.txt | grep -v amdgpu.ids ;;
+    gstamps)
+      for c in fc1gate fc1 fc2res; do
+        FERVIT_LIB=$GRAFT_REPO_ROOT/fer-vit_amd/fervit/libfervit_st.so timeout -k 10 120 python -u tools/gemm_stamps.py $c \
+          2>&1 | grep -v amdgpu.ids | sed "s/^/[$c] /" | tee -a gpurun_out/${TAG}_gemm_stamps.txt | grep -E "epilogue|prologue|steady" || exit 1
+      done ;;
     prof)
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof -o run -- \
         python3 bench.py --steps 10 --warmup 5 --no-cpu-baseline --no-traffic > gpurun_out/${TAG}_prof.json 2>&1 \
