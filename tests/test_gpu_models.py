@@ -2,8 +2,10 @@
 
 fp32 parity path: logits within 1e-3 of the reference PyTorch-CPU forward (BASELINE
 north star), argmax identical, loss, and every parameter-gradient checksum.
-bf16 fast path: same checks at bf16 tolerances (relative 5e-2), argmax on samples whose
-top-1/top-2 margin exceeds 0.2.
+bf16 fast path: the same checks with per-case gates at 2x the errors measured on the GPU
+(tools/bf16_parity_measure.py, profiles/r04o_bf16_parity.json), argmax on samples whose
+top-1/top-2 margin exceeds 0.2; and at the headline size (ViT-B/16, bs 256) bf16 logits against
+this library's fp32 parity path on identical weights and inputs.
 """
 import numpy as np
 import pytest
@@ -28,6 +30,19 @@ def build(name):
     return m.cuda(), fx
 
 
+# bf16 gates = 2x the measured max |logits - ref|, max |norm(g) - ref| / ref and max |g[i] - ref[i]| / norm(ref)
+# over the parameter gradients (profiles/r04o_bf16_parity.json: 0.0217 / 0.0030 / 0.0016 for
+# image_vit_48, 0.0216 / 0.0113 / 0.0107 vit_base_224, 0.0157 / 0.0083 / 0.0100 latent_vit,
+# 0.0290 / 0.0197 / 0.0413 latent_vit_v2_all, 0.0114 / 0.0122 / 0.0114 latent_vit_v2_lwn)
+BF16_GATES = {
+    "image_vit_48": (0.044, 0.0061, 0.0033),
+    "vit_base_224": (0.044, 0.023, 0.022),
+    "latent_vit": (0.032, 0.017, 0.021),
+    "latent_vit_v2_all": (0.058, 0.040, 0.083),
+    "latent_vit_v2_lwn": (0.023, 0.025, 0.023),
+}
+
+
 @pytest.mark.parametrize("name", list(CASES))
 @pytest.mark.parametrize("prec", ["fp32", "bf16"])
 def test_model_matches_reference(name, prec):
@@ -44,20 +59,44 @@ def test_model_matches_reference(name, prec):
         assert np.abs(lg - ref).max() < 1e-3
         assert (lg.argmax(1) == ref.argmax(1)).all()
         assert abs(loss.item() - float(fx["loss"])) < 1e-4
-        gtol = 2e-3
+        gnorm = gsamp = 2e-3
     else:
-        assert np.abs(lg - ref).max() < 5e-2 * max(1.0, np.abs(ref).max())
+        ltol, gnorm, gsamp = BF16_GATES[name]
+        assert np.abs(lg - ref).max() < ltol
         sure = fx["margin"] > 0.2
         assert (lg.argmax(1)[sure] == ref.argmax(1)[sure]).all()
-        gtol = 8e-2
     params = dict(m.named_parameters())
     for k, gl2, samp, idx in zip(fx["grad_keys"], fx["grad_l2"], fx["grad_samples"], fx["grad_idx"]):
         g = params[str(k)].grad
         assert g is not None, k
         g = g.detach().reshape(-1).double().cpu()
-        assert abs(g.norm().item() - gl2) <= gtol * gl2 + 1e-6, (k, g.norm().item(), gl2)
+        assert abs(g.norm().item() - gl2) <= gnorm * gl2 + 1e-6, (k, g.norm().item(), gl2)
         ok = idx >= 0
-        np.testing.assert_allclose(g[idx[ok]].numpy(), samp[ok], atol=gtol * gl2 + 1e-6, err_msg=str(k))
+        np.testing.assert_allclose(g[idx[ok]].numpy(), samp[ok], atol=gsamp * gl2 + 1e-6, err_msg=str(k))
+
+
+def test_bf16_headline_vs_fp32_path():
+    """ViT-B/16 at the benched size (bs 256, 224 px): the bf16 production path's logits against the
+    fp32 parity path (pinned to the reference at 1e-3 above) on identical weights and inputs, eval mode.
+    Gate: 2x the measured 0.0281 max |delta| (ref max |logit| 1.70); argmax equal where the fp32
+    top-1/top-2 margin exceeds 0.2 (144 of 256 samples in the measurement)."""
+    from models_fer_vit.image_vit import create_vit_base
+
+    torch.manual_seed(0)
+    m = create_vit_base(num_classes=7, img_size=224).cuda()
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(256, 3, 224, 224, generator=g).cuda()
+    out = {}
+    with torch.no_grad():
+        for prec in ("fp32", "bf16"):
+            m.set_precision(prec).eval()
+            out[prec] = m(x).float().cpu()
+    a, b = out["fp32"], out["bf16"]
+    assert (a - b).abs().max().item() < 0.057
+    top2 = a.topk(2, dim=1).values
+    sure = (top2[:, 0] - top2[:, 1]) > 0.2
+    assert sure.sum().item() > 64
+    assert (a.argmax(1)[sure] == b.argmax(1)[sure]).all()
 
 
 def test_eval_logits_and_no_grad():

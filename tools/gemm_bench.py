@@ -63,6 +63,11 @@ def main():
         "fc1 dgrad +res (B KC, K=3072)": (lambda: ops.linear_fwd(h, w1t, out=out_d, res=x), 2 * M * F * D, None),
         "fc1 wgrad (MN,MN splitK)": (lambda: ops.linear_wgrad(dF, x, gw), 2 * M * F * D, lambda: dF.t() @ x),
     }
+    cfg = os.environ.get("GB_CFG")  # force one tile configuration (fer_gemm_set_config)
+    if cfg is not None:
+        from fervit._lib import lib
+
+        lib().fer_gemm_set_config(int(cfg))
     only = os.environ.get("GB_ONLY")
     if only:
         cases = {k: v for k, v in cases.items() if only in k}
@@ -73,7 +78,7 @@ def main():
             res[k].append(timeit(fn))
             if tf is not None:
                 ref[k].append(timeit(tf))
-    tag = os.environ.get("FERVIT_GEMM_CFG", "auto")
+    tag = cfg if cfg is not None else "auto"
     for k, (fn, fl, tf) in cases.items():
         t = min(res[k])
         line = f"[cfg {tag}] {k:32s} ours {t * 1e3:8.1f} us  {fl / t / 1e9:7.1f} TF ({fl / t / 1e9 / PEAK * 100:4.1f}%)"
