@@ -1483,12 +1483,6 @@ template <bool AKC, bool BKC, int MT, bool DYN, int EK>
 __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmArgs g, EpiArgs e) {
   __shared__ __attribute__((aligned(1024))) char smem[8 * 16384 + 16];
   const int ntiles = g.tiles_m * g.tiles_n;
-#ifdef FER_EXP_DESYNC
-  if ((blockIdx.x & 1) && ntiles > (int)gridDim.x) {
-    const int sleeps = ((g.K + 63) / 64) * FER_EXP_DESYNC / 8192;
-    for (int i = 0; i < sleeps; ++i) __builtin_amdgcn_s_sleep(127);
-  }
-#endif
   if constexpr (!DYN) {
 #pragma unroll 1
     for (int bid = blockIdx.x; bid < ntiles; bid += gridDim.x) {
