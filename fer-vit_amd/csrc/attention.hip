@@ -318,24 +318,27 @@ __global__ __launch_bounds__(64 * (NB + 1)) void attn_fwd_pers(const bf16* __res
   // scalar offset.
   const __amdgpu_buffer_rsrc_t rq = make_rsrc(qkv), ro = make_rsrc(out), rl = make_rsrc(lse),
                                rmk = make_rsrc(mask ? (const void*)mask : (const void*)lse);
-  uint32_t q_off[4], o_off[8];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    const int d0 = 16 * s + 8 * hh;
-    q_off[s] = (q < N && d0 < dh) ? (uint32_t)(((long)q * ldq + d0) * 2) : FER_OOB;
-  }
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int d = (i >> 2) * 32 + 8 * (i & 3) + 4 * hh;
-    o_off[i] = (q < N && d < dh) ? (uint32_t)(((long)q * ldo + d) * 2) : FER_OOB;
-  }
+  // per-lane Q / O offsets recomputed where they are used (not 12 VGPRs held through the key blocks)
+  // (32-bit offsets: the host keeps qkv / out under 2 GiB; selects, not branches)
+  // (arithmetic, not a select: hipcc turned the select into two exec-masked copies of the load)
+  auto q_off = [&](int s, int ln) -> uint32_t {
+    const int qq = w * 32 + (ln & 31), d0 = 16 * s + 8 * (ln >> 5);
+    const uint32_t off = ((uint32_t)qq * (uint32_t)ldq + (uint32_t)d0) * 2u;
+    return off | ((uint32_t)(qq >= N || d0 >= dh) << 31);  // bit 31 set: past the range (FER_OOB)
+  };
+  auto o_off = [&](int i, int ln) -> uint32_t {
+    const int qq = w * 32 + (ln & 31), d = (i >> 2) * 32 + 8 * (i & 3) + 4 * (ln >> 5);
+    const uint32_t off = ((uint32_t)qq * (uint32_t)ldo + (uint32_t)d) * 2u;
+    return off | ((uint32_t)(qq >= N || d >= dh) << 31);
+  };
   const uint32_t lse_off = (q < N && hh == 0) ? (uint32_t)(q * 4) : FER_OOB;
   const uint32_t mk_off = (mask && lane < 32) ? (uint32_t)(lane * 4) : FER_OOB;
   auto load_q = [&](bf16x8 (&qv)[4], int unit) {
     const int b = unit / H, h = unit - b * H;
     const int so = __builtin_amdgcn_readfirstlane((int)((((long)b * N) * ldq + h * dh) * 2));
 #pragma unroll
-    for (int s = 0; s < 4; ++s) qv[s] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rq, q_off[s], so, 0));
+    for (int s = 0; s < 4; ++s)
+      qv[s] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rq, q_off(s, lane), so, 0));
   };
   // units: fixed stride, or the work queue `wq` (common.h): the first unit is blockIdx.x, the next
   // one is claimed at the start, then the producer's lane 0 claims the unit after next while this
@@ -349,7 +352,8 @@ __global__ __launch_bounds__(64 * (NB + 1)) void attn_fwd_pers(const bf16* __res
     u = blockIdx.x;
     un = u + (int)gridDim.x < BH ? u + (int)gridDim.x : -1;
   }
-  bf16x8 qf[4];
+  // producer and compute waves run separate unit loops with the same barriers (prologue + one per
+  // unit) and hand-off reads: a loop shared by both roles merged their register states at its latch
   if (w == NB) {
     uint32_t c0 = 0;
     if (wq.q && claimer) c0 = wq_claim_issue(wq.q);  // its round trip overlaps the DMA wait
@@ -357,19 +361,15 @@ __global__ __launch_bounds__(64 * (NB + 1)) void attn_fwd_pers(const bf16* __res
     wait_vm<0>();
     asm volatile("" : "+v"(c0));
     if (wq.q && claimer) hand[2] = wq_claim_finish(c0, wq.base, BH);
-  } else {
-    load_q(qf, u);
-  }
-  bar_lds();
-  if (wq.q) un = __builtin_amdgcn_readfirstlane(hand[2]);
+    bar_lds();
+    if (wq.q) un = __builtin_amdgcn_readfirstlane(hand[2]);
 #pragma unroll 1
-  for (int k = 0;; ++k) {
+    for (int k = 0;; ++k) {
 #ifdef FER_ATTN_STAMPS
-    const bool st_on = blockIdx.x == 0 && (k == 2 || k == 3);
-    const int sb = (k - 2) * 32;
+      const bool st_on = blockIdx.x == 0 && (k == 2 || k == 3);
+      const int sb = (k - 2) * 32;
 #endif
-    AST(sb + 0);
-    if (w == NB) {
+      AST(sb + 0);
       int unn = -1;
       uint32_t craw = 0;
       if (wq.q) {
@@ -384,11 +384,32 @@ __global__ __launch_bounds__(64 * (NB + 1)) void attn_fwd_pers(const bf16* __res
       asm volatile("" : "+v"(craw));
       if (wq.q && claimer && un >= 0) unn = wq_claim_finish(craw, wq.base, BH);
       if (claimer) hand[k & 1] = unn;
-    } else {
+      bar_lds();  // the DMA of unit un has landed (wait_vm above); every wave is done with unit u
+      AST(sb + 21);
+      u = un;
+      un = __builtin_amdgcn_readfirstlane(hand[k & 1]);
+      if (u < 0) break;
+    }
+    return;
+  }
+  bf16x8 qf[4];
+  load_q(qf, u);
+  // consumed here: the first unit's loads complete before the loop, so the loop header's wait state
+  // (merged over this entry and the back edge) keeps the back edge's count -- Q issued before the
+  // previous unit's 9 output stores -- instead of waiting for those stores too
+  asm volatile("" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3]));
+  bar_lds();
+  if (wq.q) un = __builtin_amdgcn_readfirstlane(hand[2]);
+#pragma unroll 1
+  for (int k = 0;; ++k) {
+#ifdef FER_ATTN_STAMPS
+    const bool st_on = blockIdx.x == 0 && (k == 2 || k == 3);
+    const int sb = (k - 2) * 32;
+#endif
+    AST(sb + 0);
+    {
       const char* Ki = lds + (k & 1) * 2 * IMG;
       const char* Vi = Ki + IMG;
-      bf16x8 qn[4];
-      if (un >= 0) load_q(qn, un);
       const int bh = u, b = u / H, h = u - b * H;
       const uint32_t row = drop_row(bh, N, q);
       float m = -INFINITY, l = 0.f;
@@ -466,6 +487,10 @@ __global__ __launch_bounds__(64 * (NB + 1)) void attn_fwd_pers(const bf16* __res
         block(kb, st, vfr);
         AST(sb + 2 + 2 * kb);
       }
+      // the next unit's Q straight into qf (dead after the last key block): issued ahead of the output
+      // stores, so its wait at the next unit's first key block skips them; unconditional (un < 0: this
+      // unit's again), so the loop carries one version of qf
+      load_q(qf, un >= 0 ? un : u);
       l = xhalf_sum(l);
       {
         const float mul = dscale / l;
@@ -476,13 +501,11 @@ __global__ __launch_bounds__(64 * (NB + 1)) void attn_fwd_pers(const bf16* __res
           const int g4 = i & 3;
           const bf16x4 v = {(bf16)(a[4 * g4] * mul), (bf16)(a[4 * g4 + 1] * mul), (bf16)(a[4 * g4 + 2] * mul),
                             (bf16)(a[4 * g4 + 3] * mul)};
-          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), ro, o_off[i], so, 0);
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), ro, o_off(i, lane), so, 0);
         }
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint((m + log2f(l)) * LN2), rl, lse_off,
                                               __builtin_amdgcn_readfirstlane(bh * N * 4), 0);
       }
-#pragma unroll
-      for (int s = 0; s < 4; ++s) qf[s] = qn[s];
       AST(sb + 20);
     }
     bar_lds();  // the producer's DMA of unit un has landed (its wait_vm); every wave is done with unit u
@@ -964,7 +987,10 @@ __global__ __launch_bounds__(64 * NB) void attn_bwd_pers(
         // issued: the DMA is inline asm, invisible to the compiler's wait counts, so its vmcnt(0) for
         // the word would otherwise wait for the DMA as well
         // bit acc_row(r, 0) = keep of query row r
-        const uint32_t mws = (FIRST ? mwn : (mask ? mwn : 0xFFFFFFFFu)) >> (4 * hh);
+        uint32_t mws = (FIRST ? mwn : (mask ? mwn : 0xFFFFFFFFu)) >> (4 * hh);
+        // pinned here: left to the compiler, the select sank below the LAST step's loads of the next
+        // unit (and its exec-masked claim atomic) and waited vmcnt(0) for all of them (~4k cycles/unit)
+        asm volatile("" : "+v"(mws)::"memory");
         if (i == 0 && has_next) prep_issue(un, cur ^ 1);
         int qb = w + i;
         if (qb >= NB) qb -= NB;
