@@ -213,12 +213,13 @@ FER_DEV void epi8_t(const EpiArgs& e, long m, long n, f32x4& v0, f32x4& v1, f32x
 // the dropout scale folded into constants: GATE takes it in the GELU constants (gelu_and_grad8s),
 // RES as acc * (alpha*s) + b*s (ab = alpha*s, b0 / b1 pre-scaled by the caller), so a dropped
 // element costs a select only.
-// Outputs go out as buffer stores at byte offsets ocb / opb (FER_OOB for a row out of range: the
-// store is dropped without a branch, so the compiler's wait counts around it stay exact).
+// Returns the output row piece; GATE / GATER also the pre-activation gate piece (`gp`). The caller
+// stores them (pointer stores behind the row check in the shared staged loop -- buffer stores there
+// made the 128^2 kernel's STORE / MUL kinds 50-80 % slower on the latent shapes, profiles/r04z_* --
+// buffer stores with FER_OOB rows in the 8-phase kernel's register-fed and wave-private paths).
 template <int S0>
-FER_DEV void epi8_k(const EpiArgs& e, uint32_t ocb, uint32_t opb, uint32_t di, f32x4& v0, f32x4& v1, f32x4 b0,
-                    f32x4 b1, bf16x8 x, uint64_t seed, float ab, f32x2 ghs, f32x2 gps, float dsr,
-                    const __amdgpu_buffer_rsrc_t& rc, const __amdgpu_buffer_rsrc_t& rp) {
+FER_DEV bf16x8 epi8_k(const EpiArgs& e, uint32_t di, f32x4& v0, f32x4& v1, f32x4 b0, f32x4 b1, bf16x8 x,
+                      uint64_t seed, float ab, f32x2 ghs, f32x2 gps, float dsr, bf16x8& gp) {
   constexpr int S = epi_base(S0);
   static_assert(S != EPI_GEN, "generic epilogue goes through epi8_t");
   v0 = v0 * ab + b0;
@@ -235,7 +236,7 @@ FER_DEV void epi8_k(const EpiArgs& e, uint32_t ocb, uint32_t opb, uint32_t di, f
       v0[r] = k0 ? fmaxf(v0[r], 0.f) : 0.f;
       v1[r] = k1 ? fmaxf(v1[r], 0.f) : 0.f;
     }
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, pack8(g0, g1)), rp, opb, 0, 0);
+    gp = pack8(g0, g1);
   }
   if constexpr (S == EPI_GATE) {
     f32x4 g0, g1;
@@ -254,7 +255,7 @@ FER_DEV void epi8_k(const EpiArgs& e, uint32_t ocb, uint32_t opb, uint32_t di, f
         g1[r] = kp[4 + r] ? g1[r] : 0.f;
       }
     }
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, pack8(g0, g1)), rp, opb, 0, 0);
+    gp = pack8(g0, g1);
   }
   if constexpr (S == EPI_RES) {
     if (e.drop_thresh) {
@@ -273,7 +274,20 @@ FER_DEV void epi8_k(const EpiArgs& e, uint32_t ocb, uint32_t opb, uint32_t di, f
     v0 *= lo4(x);
     v1 *= hi4(x);
   }
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, pack8(v0, v1)), rc, ocb, 0, 0);
+  return pack8(v0, v1);
+}
+// epi8_k + buffer stores at byte offsets ocb / opb (FER_OOB for a row out of range: dropped without a
+// branch, so the compiler's wait counts around them stay exact)
+template <int S0>
+FER_DEV void epi8_kb(const EpiArgs& e, uint32_t ocb, uint32_t opb, uint32_t di, f32x4& v0, f32x4& v1, f32x4 b0,
+                     f32x4 b1, bf16x8 x, uint64_t seed, float ab, f32x2 ghs, f32x2 gps, float dsr,
+                     const __amdgpu_buffer_rsrc_t& rc, const __amdgpu_buffer_rsrc_t& rp) {
+  constexpr int S = epi_base(S0);
+  bf16x8 gp;
+  const bf16x8 o = epi8_k<S0>(e, di, v0, v1, b0, b1, x, seed, ab, ghs, gps, dsr, gp);
+  if constexpr (S == EPI_GATE || S == EPI_GATER)
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, gp), rp, opb, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), rc, ocb, 0, 0);
 }
 
 // kind for a launch (EPI_GEN unless every flag matches one of the fixed kinds)
@@ -589,6 +603,7 @@ FER_DEV void tile_epilogue(const GemmArgs& g, const EpiArgs& e, AccT (&acc)[FN][
   const void* xs = e.res ? e.res : e.aux;  // the row operand brought in by DMA
   const long ldxs = e.res ? e.ldr : e.ldx;
   const __amdgpu_buffer_rsrc_t rx = make_rsrc(xs), rc = make_rsrc(e.c), rp = make_rsrc(e.pre ? e.pre : e.c);
+  (void)rp;
   // this lane's DMA source for piece k of chunk 0 (rows advance by EROWS per chunk)
   const int xrow = lane / LPR, xcol = (lane % LPR) * 8;
   const bool xcol_ok = n0 + xcol + 8 <= g.N;
@@ -650,16 +665,15 @@ FER_DEV void tile_epilogue(const GemmArgs& g, const EpiArgs& e, AccT (&acc)[FN][
       const long m = m0 + h * EROWS + r;
       f32x4 v0 = *(const f32x4*)(stg + swz(r, tc)), v1 = *(const f32x4*)(stg + swz(r, tc + 4));
       const bf16x8 x = xs ? *(const bf16x8*)(xh + (r * BN + tc) * 2) : bf16x8{};
-      const bool ok = nok && m < g.M;
-      if constexpr (KIND) {
-        epi8_k<EK>(e, ok ? (uint32_t)(oc * 2) : FER_OOB, ok ? (uint32_t)(op * 2) : FER_OOB, di, v0, v1, b0, b1, x,
-                   seed, ab, ghs, gps, dsc, rc, rp);
-        if constexpr (CS) {
-          cs0 += ok ? v0 : f32x4{0.f, 0.f, 0.f, 0.f};
-          cs1 += ok ? v1 : f32x4{0.f, 0.f, 0.f, 0.f};
+      if (nok && m < g.M) {
+        if constexpr (KIND) {
+          bf16x8 gp;
+          const bf16x8 o = epi8_k<EK>(e, di, v0, v1, b0, b1, x, seed, ab, ghs, gps, dsc, gp);
+          if constexpr (epi_base(EK) == EPI_GATE || EK == EPI_GATER) *(bf16x8*)((bf16*)e.pre + op) = gp;
+          *(bf16x8*)((bf16*)e.c + oc) = o;
+        } else {
+          epi8_t<EK>(e, m, n, v0, v1, b0, b1, x, ps, seed);
         }
-      } else if (ok) {
-        epi8_t<EK>(e, m, n, v0, v1, b0, b1, x, ps, seed);
         if constexpr (CS) {
           cs0 += v0;
           cs1 += v1;
@@ -700,7 +714,7 @@ FER_DEV void tile_epilogue(const GemmArgs& g, const EpiArgs& e, AccT (&acc)[FN][
           n1 = *(const f32x4*)(stg + swz(r + RPI, tc + 4));
         }
         const bool ok = nok && m < g.M;
-        epi8_k<EK>(e, ok ? (uint32_t)m * ldcb + (uint32_t)n * 2 : FER_OOB, FER_OOB,
+        epi8_kb<EK>(e, ok ? (uint32_t)m * ldcb + (uint32_t)n * 2 : FER_OOB, FER_OOB,
                    di0 + (uint32_t)(it * RPI) * (uint32_t)e.drop_ld, v0, v1, b0, b1, xr[it], seed, ab, ghs, gps, dsc,
                    rc, rp);
         if constexpr (CS) {
@@ -1296,7 +1310,7 @@ FER_DEV void tile_epilogue_wp(const GemmArgs& g, const EpiArgs& e, f32x4 (&acc)[
       const int row = rw0 + c * 32 + p * 8;
       const bool ok = nok && row < g.M;
       const uint32_t di = (uint32_t)row * (uint32_t)e.drop_ld + (uint32_t)n;
-      epi8_k<EK>(e, ok ? (uint32_t)row * ldcb + (uint32_t)n * 2 : FER_OOB,
+      epi8_kb<EK>(e, ok ? (uint32_t)row * ldcb + (uint32_t)n * 2 : FER_OOB,
                  ok ? (uint32_t)row * ldpb + (uint32_t)n * 2 : FER_OOB, di, v0, v1, b0, b1,
                  X ? xr[c & 1][p] : bf16x8{}, seed, ab, ghs, gps, dsc, rc, rp);
       if constexpr (CS) {
