@@ -1311,8 +1311,8 @@ FER_DEV void tile_epilogue_wp(const GemmArgs& g, const EpiArgs& e, f32x4 (&acc)[
       const bool ok = nok && row < g.M;
       const uint32_t di = (uint32_t)row * (uint32_t)e.drop_ld + (uint32_t)n;
       epi8_kb<EK>(e, ok ? (uint32_t)row * ldcb + (uint32_t)n * 2 : FER_OOB,
-                 ok ? (uint32_t)row * ldpb + (uint32_t)n * 2 : FER_OOB, di, v0, v1, b0, b1,
-                 X ? xr[c & 1][p] : bf16x8{}, seed, ab, ghs, gps, dsc, rc, rp);
+                  ok ? (uint32_t)row * ldpb + (uint32_t)n * 2 : FER_OOB, di, v0, v1, b0, b1,
+                  X ? xr[c & 1][p] : bf16x8{}, seed, ab, ghs, gps, dsc, rc, rp);
       if constexpr (CS) {
         cs0 += ok ? v0 : f32x4{0.f, 0.f, 0.f, 0.f};
         cs1 += ok ? v1 : f32x4{0.f, 0.f, 0.f, 0.f};
@@ -1934,10 +1934,12 @@ int gemm_launch(const GemmDesc& d, const EpiArgs& e_in, hipStream_t st) {
     return (int)std::max<long>(1, std::min<long>({target / tiles, d.K / 256, (long)max_splits}));
   };
   // split targets (workgroups per launch) of the 256^2 / 128^2 tile configs
-  // (MN x MN weight gradients: 192 workgroups, not one per CU -- they run beside the compute stream,
-  // and leaving it CUs took the ViT-B step 36.06-36.33 -> 35.81-36.02 ms; 128 is 39 ms: the last
-  // layers' weight gradients then form a long tail; profiles/r03aa_wgrad_split_target_ab.txt)
-  constexpr long tgt256 = 256, tgt256_mn = 192;
+  // (MN x MN weight gradients: 224 workgroups, not one per CU -- they run beside the compute stream,
+  // and leaving it CUs took the ViT-B step 36.06-36.33 -> 35.81-36.02 ms at 192; 128 is 39 ms: the last
+  // layers' weight gradients then form a long tail; profiles/r03aa_wgrad_split_target_ab.txt. With the
+  // round-4 compute-stream kernels 224 is 35.91 / 35.92 vs 192 35.98 / 36.04 and 160 36.04 / 36.07 ms,
+  // profiles/r04ac_wgrad_split_target_ab.txt)
+  constexpr long tgt256 = 256, tgt256_mn = 224;
   // (128^2, K-contiguous: split only below half a round; the ordered slab reduction costs more than the
   // idle CUs of an unsplit 152-228 tile grid -- latent fc2 fwd 50.7 -> 29.4 us, qkv dgrad 46.4 -> 22.9 us)
   const long tgt128k = (d.a_kc && d.b_kc) ? 256 : 512;
