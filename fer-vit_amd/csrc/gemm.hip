@@ -1485,6 +1485,234 @@ FER_DEV void tile_8ph(const GemmArgs& g, const EpiArgs& e, int bid, char* smem, 
 #endif
 }
 
+// ---- Pipelined schedule for the plain kind (EPI_STORE, MT 16): a tile's epilogue overlaps the next
+// tile's first operand loads and its own store drain overlaps the next tile's first K-tile.
+// vmcnt retires in issue order, so in the plain schedule (epilogue stores, then the next tile's
+// prologue DMA and its wait) every tile start waits for the previous tile's stores to reach memory
+// and then for a full DMA round trip. Here the workgroup issues the next tile's prologue (pro_8ph:
+// A0 B0 A1 B1 of K-tile 0 and A0 of K-tile 1, ten instructions per wave) right after its main loop,
+// BEFORE the epilogue; the epilogue stages through stage 1's B units (free until K-tile 1's B0
+// issue, which comes after the epilogue's closing barrier), and the next tile's first two waits
+// skip the epilogue's PP_SV vector-memory instructions (its 16 buffer stores per wave, issued
+// unconditionally at FER_OOB offsets; anything the compiler adds only makes those waits stricter),
+// which are younger than the operands they wait for. The first wait covering them is K-tile 1's.
+// Measured (profiles/r04ah_gemm_pipelined_store_ab.txt, same box, against the plain schedule):
+// fc1-shape fwd 237.4 -> 224.7 us (+bias 231.9 -> 221.2), qkv fwd 167.0 -> 163.7, the transposed-
+// copy fc2 dgrad 229.3 -> 226.1; K = 3072 (fc2 fwd) unchanged. (A first version lost most of it:
+// alpha / bias read through the EpiArgs reference were kept in a per-thread copy the compiler
+// promoted to LDS, and that read waited vmcnt(0) for the LDS DMA -- r04ag.) The row-operand and
+// gate kinds stay on tile_8ph: this schedule for them (gpurun_out/patches/
+// gemm_pipelined_all_kinds.patch) faulted the GPU on its first residual launch (M 20000, N 3000,
+// K 520; profiles/r04af_pipelined_all_kinds_fault_ktests.txt), cause not found.
+constexpr int PP_SV = 16;
+
+// Always exactly ten instructions per wave, without a branch (the epilogue's compiler-placed waits
+// for its bias loads would otherwise merge the issue and no-issue paths into a
+// vmcnt(0), i.e. wait for this DMA): bid < 0 (no next tile) or units beyond K go to FER_OOB, whose
+// LDS writes land in stage 0 and stage 1's A0 unit, which the epilogue does not use.
+template <bool AKC, bool BKC, int MT, int EK>
+FER_DEV void pro_8ph(const GemmArgs& g, int bid, char* smem, int wave, int lane) {
+  constexpr int UNIT = 16384, BUF = 4 * UNIT;
+  int tm, tn;
+  tile_of(bid < 0 ? 0 : bid, g.tiles_m, g.tiles_n, tm, tn, EK == EPI_GATE ? 4 : 8);
+  const int kbeg = blockIdx.y * g.k_chunk, kend = bid < 0 ? kbeg : min(g.K, kbeg + g.k_chunk);
+  const int ktail = kbeg + ((kend - kbeg + 63) / 64 - 1) * 64;
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(g.A), rb = make_rsrc(g.B);
+  UnitPlan<AKC, MT, true> a0, a1;
+  UnitPlan<BKC, MT, false> b0, b1;
+  a0.init(wave, lane, g.lda, tm * 256, g.M, 0);
+  a1.init(wave, lane, g.lda, tm * 256, g.M, 1);
+  b0.init(wave, lane, g.ldb, tn * 256, g.N, 0);
+  b1.init(wave, lane, g.ldb, tn * 256, g.N, 1);
+  // (tail: every unit at or past the last K-tile checks its columns against kend)
+  a0.issue(ra, smem, wave, g.lda, kbeg, kend, kbeg >= ktail);
+  b0.issue(rb, smem + 2 * UNIT, wave, g.ldb, kbeg, kend, kbeg >= ktail);
+  a1.issue(ra, smem + UNIT, wave, g.lda, kbeg, kend, kbeg >= ktail);
+  b1.issue(rb, smem + 3 * UNIT, wave, g.ldb, kbeg, kend, kbeg >= ktail);
+  a0.issue(ra, smem + BUF, wave, g.lda, kbeg + 64, kend, kbeg + 64 >= ktail);
+}
+
+// The pipelined schedule's epilogue (EPI_STORE: c = alpha acc + bias), with the next tile's prologue
+// issued after the bias loads. Each wave stages its 128 x 64 region through its own 4 KB of stage
+// 1's B units, eight 16-row chunks of fp32 XOR-swizzled by row, read back row-contiguous (lane =
+// row lane >> 3 of an 8-row pass, columns 8 (lane & 7)): 16-byte buffer stores, whole 128-byte
+// rows per 8 lanes, FER_OOB for rows past M.
+// (the epilogue fields arrive as values, PpEpi: reading them through the EpiArgs reference left
+// alpha and bias in a per-thread copy that the compiler promoted to LDS, whose read then waited
+// vmcnt(0) for the in-flight LDS DMA)
+struct PpEpi {
+  void* c;
+  const float* bias;
+  long ldc;
+  float alpha;
+};
+template <bool AKC, bool BKC, int MT>
+FER_DEV void epi_8ph_pp(const GemmArgs& g, const PpEpi& e, f32x4 (&acc)[4][8], char* smem, int m0, int n0, int wave,
+                        int lane, int next) {
+  constexpr int UNIT = 16384, BUF = 4 * UNIT;
+  const int wr = wave >> 2, wc = wave & 3;
+  const int prow = lane >> 3, pc = 8 * (lane & 7);
+  const int n = n0 + wc * 64 + pc;
+  const bool nok = n < g.N;  // N % 8 == 0 on this path (checked by the host)
+  const __amdgpu_buffer_rsrc_t rbias = make_rsrc(e.bias ? (const void*)e.bias : e.c);
+  const uint32_t boff = (e.bias && nok) ? (uint32_t)n * 4 : FER_OOB;
+  const f32x4 b0 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rbias, boff, 0, 0));
+  const f32x4 b1 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rbias, boff + 16, 0, 0));
+  pro_8ph<AKC, BKC, MT, EPI_STORE>(g, next, smem, wave, lane);
+  const __amdgpu_buffer_rsrc_t rc = make_rsrc(e.c);
+  const uint32_t ldcb = (uint32_t)e.ldc * 2;
+  const float alpha = e.alpha;
+  const int rw0 = m0 + wr * 128 + prow;  // this lane's row in pass 0 of chunk 0
+  char* const ws = smem + BUF + 2 * UNIT + wave * 4096;
+  auto swz = [](int row, int c16) { return row * 256 + ((c16 ^ row) << 4); };
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) *(f32x4*)(ws + swz(lane & 15, 4 * i + (lane >> 4))) = acc[i][c];
+    // (a wave's own LDS accesses complete in order: no barrier)
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int lrow = p * 8 + prow;
+      const f32x4 v0 = *(const f32x4*)(ws + swz(lrow, pc >> 2)) * alpha + b0;
+      const f32x4 v1 = *(const f32x4*)(ws + swz(lrow, (pc >> 2) + 1)) * alpha + b1;
+      const int row = rw0 + c * 16 + p * 8;
+      const uint32_t oc = (nok && row < g.M) ? (uint32_t)row * ldcb + (uint32_t)n * 2 : FER_OOB;
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, pack8(v0, v1)), rc, oc, 0, 0);
+    }
+  }
+  bar_lds();  // the staging area is K-tile 1's B units
+}
+
+// One tile of the pipelined schedule; returns the workgroup's next tile (-1: none). PEND: the
+// previous tile's epilogue sits between this tile's prologue DMA and its first wait (every tile
+// but a workgroup's first; a template flag: as a loop-carried bool it took a VGPR that spilled).
+template <bool AKC, bool BKC, int MT, int EK, bool PEND>
+FER_DEV int tile_8ph_pp(const GemmArgs& g, const PpEpi& e, int bid, char* smem, lds_vint* slot) {
+  static_assert(MT == 16 && EK == EPI_STORE, "pipelined schedule: MT 16 fragments, plain kind");
+  constexpr int UNIT = 16384, BUF = 4 * UNIT;
+  constexpr int FM = 8, FN = 4, QJ = 4, QI = 2, KS = 2;
+  constexpr int SV = PP_SV;
+  int tid = threadIdx.x;
+  asm volatile("" : "+v"(tid));
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+
+  int tm, tn;
+  tile_of(bid, g.tiles_m, g.tiles_n, tm, tn, EK == EPI_GATE ? 4 : 8);
+  const int m0 = tm * 256, n0 = tn * 256;
+  const int kbeg = blockIdx.y * g.k_chunk;
+  const int kend = min(g.K, kbeg + g.k_chunk);
+  const int nk = (kend - kbeg + 63) / 64;
+  const int ktail = kbeg + (nk - 1) * 64;
+
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(g.A);
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(g.B);
+  UnitPlan<AKC, MT, true> pa0, pa1;
+  UnitPlan<BKC, MT, false> pb0, pb1;
+  pa0.init(wave, lane, g.lda, m0, g.M, 0);
+  pa1.init(wave, lane, g.lda, m0, g.M, 1);
+  pb0.init(wave, lane, g.ldb, n0, g.N, 0);
+  pb1.init(wave, lane, g.ldb, n0, g.N, 1);
+  auto unit = [&](int T, int u) -> char* { return smem + (T & 1) * BUF + u * UNIT; };
+  auto kt = [&](int T) { return kbeg + T * 64; };
+  auto iA0 = [&](int T) { pa0.issue(ra, unit(T, 0), wave, g.lda, kt(T), kend, kt(T) == ktail); };
+  auto iA1 = [&](int T) { pa1.issue(ra, unit(T, 1), wave, g.lda, kt(T), kend, kt(T) == ktail); };
+  auto iB0 = [&](int T) { pb0.issue(rb, unit(T, 2), wave, g.ldb, kt(T), kend, kt(T) == ktail); };
+  auto iB1 = [&](int T) { pb1.issue(rb, unit(T, 3), wave, g.ldb, kt(T), kend, kt(T) == ktail); };
+
+  f32x4 acc[FN][FM];
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int j = 0; j < FM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 fa[2][KS][QJ], fb[2][KS][QI];
+
+  // The next tile's claim, read after the main loop (whose last K-tile waits for vmcnt(0)). Inline
+  // asm (wq_claim_issue): the builtin atomic's result is consumed at once, a vmcnt(0) that would
+  // wait for the previous epilogue's stores. In wave 0 it adds one younger instruction to the
+  // first two waits, which then also wait for one more DMA instruction.
+  uint32_t claim_raw = 0;
+  if (slot && tid == 0) {
+    // (the queue word's address in SGPRs: a VGPR pair kept across the main loop spilled)
+    const int* qp = g.tq + (blockIdx.x & 7) * FER_WQ_PAD;
+    asm volatile("global_atomic_add %0, %1, %2, %3 sc0" : "=v"(claim_raw) : "v"(0u), "v"(1), "s"(qp) : "memory");
+  }
+  if (nk > 0) {
+    // A0, B0 of K-tile 0 (pro_8ph always issues five units)
+    if constexpr (PEND) wait_vm<6 + SV>(); else wait_vm<6>();
+    __builtin_amdgcn_s_barrier();
+    if (wr) __builtin_amdgcn_s_barrier();  // stagger: waves 4-7 one barrier behind
+    asm volatile("" ::: "memory");
+  }
+
+  for (int T = 0; T < nk; ++T) {
+    const bool n1 = T + 1 < nk, n2 = T + 2 < nk;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (q < 2) {
+        const char* ua = unit(T, q);
+        const char* ub = unit(T, 2 + q);
+#pragma unroll
+        for (int kk = 0; kk < KS; ++kk)
+#pragma unroll
+          for (int i = 0; i < QI; ++i) fb[q][kk][i] = read_frag<MT, 128, BKC, 64>(ub, wc * 32 + i * MT, kk, lane);
+#pragma unroll
+        for (int kk = 0; kk < KS; ++kk)
+#pragma unroll
+          for (int j = 0; j < QJ; ++j) fa[q][kk][j] = read_frag<MT, 128, AKC, 64>(ua, wr * 64 + j * MT, kk, lane);
+      }
+      if (q == 0) {
+        if (n1) {
+          iB0(T + 1);
+          if (PEND && T == 0) wait_vm<4 + SV>(); else wait_vm<4>();
+        } else {
+          wait_vm<0>();
+        }
+      } else if (q == 1) {
+        if (n1) iA1(T + 1);
+      } else if (q == 2) {
+        if (n1) iB1(T + 1);
+      } else {
+        if (n2) { iA0(T + 2); wait_vm<6>(); } else if (n1) { wait_vm<4>(); }
+      }
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      const int qm = (q == 0 || q == 2) ? 0 : 1;
+      const int qn = (q == 0 || q == 3) ? 0 : 1;
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int kk = 0; kk < KS; ++kk)
+#pragma unroll
+        for (int j = 0; j < QJ; ++j)
+#pragma unroll
+          for (int i = 0; i < QI; ++i)
+            acc[qn * QI + i][qm * QJ + j] = mfma<MT>(fb[qn][kk][i], fa[qm][kk][j], acc[qn * QI + i][qm * QJ + j]);
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
+  }
+  if (slot && tid == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (already retired by the last K-tile's wait)
+    asm volatile("" : "+v"(claim_raw));
+    *slot = claim_raw;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  if (nk > 0 && !wr) __builtin_amdgcn_s_barrier();  // waves 0-3 catch up with the stagger
+  int next;
+  if (slot) {
+    next = wq_claim_finish((uint32_t)__builtin_amdgcn_readfirstlane(*slot), g.tq_base, g.tiles_m * g.tiles_n);
+  } else {
+    next = bid + (int)gridDim.x;
+    if (next >= g.tiles_m * g.tiles_n) next = -1;
+  }
+
+  epi_8ph_pp<AKC, BKC, MT>(g, e, acc, smem, m0, n0, wave, lane, next);
+  return next;
+}
+
 // Persistent launch (one workgroup per CU, tiles bid, bid + grid, ...: the XCD-aware tile order
 // is kept since grid % 8 == 0). A workgroup goes from one tile's epilogue stores straight into
 // the next tile's operand DMA, so the store drain overlaps the next tile's first loads instead
@@ -1497,7 +1725,20 @@ template <bool AKC, bool BKC, int MT, bool DYN, int EK>
 __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmArgs g, EpiArgs e) {
   __shared__ __attribute__((aligned(1024))) char smem[8 * 16384 + 16];
   const int ntiles = g.tiles_m * g.tiles_n;
-  if constexpr (!DYN) {
+  if constexpr (EK == EPI_STORE && MT == 16) {
+    lds_vint* slot = DYN ? FER_LDS_INT(smem + 8 * 16384) : nullptr;
+    int bid = DYN ? wq_first(ntiles) : ((int)blockIdx.x < ntiles ? (int)blockIdx.x : -1);
+    if (bid < 0) return;
+    {
+      int tid = threadIdx.x;
+      asm volatile("" : "+v"(tid));
+      pro_8ph<AKC, BKC, MT, EK>(g, bid, smem, __builtin_amdgcn_readfirstlane(tid >> 6), tid & 63);
+    }
+    const PpEpi pe{e.c, e.bias, (long)e.ldc, e.alpha};
+    bid = tile_8ph_pp<AKC, BKC, MT, EK, false>(g, pe, bid, smem, slot);
+#pragma unroll 1
+    while (bid >= 0) bid = tile_8ph_pp<AKC, BKC, MT, EK, true>(g, pe, bid, smem, slot);
+  } else if constexpr (!DYN) {
 #pragma unroll 1
     for (int bid = blockIdx.x; bid < ntiles; bid += gridDim.x) {
       tile_8ph<AKC, BKC, MT, EK>(g, e, bid, smem, nullptr);
