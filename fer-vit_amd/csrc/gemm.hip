@@ -447,14 +447,19 @@ struct DmaPlan {
       base[i] = ok ? off : FER_OOB;
     }
   }
-  FER_DEV void issue(__amdgpu_buffer_rsrc_t rs, char* lds_tile, int wave, long ld, int k0, int kmax,
-                     bool tail) const {
+  // Inline-asm DMA (common.h dma16_asm): with the builtin, the compiler's wait-count pass put an
+  // s_waitcnt vmcnt(0) in front of the fragment reads of every K-step of the MN-operand kernels (it
+  // cannot tell a ds_read_b64_tr_b16 from the DMA's target), i.e. waited for the stages still in
+  // flight. The issuing waves' counted waits (wait_vm) stay as they are. Measured neutral (fc1 weight
+  // gradient alone 275.7 vs 274.1 us, the step 35.97-36.11 vs 36.01-36.08 ms on one box:
+  // profiles/r04aj_asm_dma_gemm_ab.txt, r04ak_asm_dma_step_ab.txt): two stages in flight already
+  // covered the DMA latency; kept so the prefetch depth is the one the code states.
+  FER_DEV void issue(const u32x4& rs, char* lds_tile, int wave, long ld, int k0, int kmax, bool tail) const {
     const uint32_t kadd = KC ? (uint32_t)(k0 * 2) : (uint32_t)(k0 * ld * 2);
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
       const uint32_t voff = (!tail || k0 + kof[i] < kmax) ? base[i] + kadd : FER_OOB;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(lds_tile + (wave * NI + i) * 1024), 16, voff, 0, 0,
-                                               0);
+      dma16_asm(lds_tile + (wave * NI + i) * 1024, rs, voff);
     }
   }
 };
@@ -856,8 +861,8 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g, 
   const int kend = min(g.K, kbeg + g.k_chunk);
   const int nk = (kend - kbeg + BK - 1) / BK;
 
-  const __amdgpu_buffer_rsrc_t ra = make_rsrc(g.A);
-  const __amdgpu_buffer_rsrc_t rb = make_rsrc(g.B);
+  const u32x4 ra = rsrc4(g.A);
+  const u32x4 rb = rsrc4(g.B);
   DmaPlan<BM, AKC, NW, MT> pa;
   DmaPlan<BN, BKC, NW, MT> pb;
   pa.init(wave, lane, g.lda, m0, g.M);
@@ -962,8 +967,8 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_ring_kernel(GemmArgs g, 
   const int kend = min(g.K, kbeg + g.k_chunk);
   const int nk = (kend - kbeg + RBK - 1) / RBK;
 
-  const __amdgpu_buffer_rsrc_t ra = make_rsrc(g.A);
-  const __amdgpu_buffer_rsrc_t rb = make_rsrc(g.B);
+  const u32x4 ra = rsrc4(g.A);
+  const u32x4 rb = rsrc4(g.B);
   typedef DmaPlan<BM, AKC, NW, MT, RBK> PA;
   typedef DmaPlan<BN, BKC, NW, MT, RBK> PB;
   PA pa;
@@ -1083,8 +1088,8 @@ __global__ __launch_bounds__(256, 2) void gemm_pp_kernel(GemmArgs g, EpiArgs e) 
   const int kend = min(g.K, kbeg + g.k_chunk);
   const int nk = (kend - kbeg + RBK - 1) / RBK;
   const int ktail = kbeg + (nk - 1) * RBK;
-  const __amdgpu_buffer_rsrc_t ra = make_rsrc(g.A);
-  const __amdgpu_buffer_rsrc_t rb = make_rsrc(g.B);
+  const u32x4 ra = rsrc4(g.A);
+  const u32x4 rb = rsrc4(g.B);
   typedef DmaPlan<BM, AKC, NW, MT, RBK> PA;
   typedef DmaPlan<BN, BKC, NW, MT, RBK> PB;
   PA pa;
@@ -1867,8 +1872,8 @@ __global__ __launch_bounds__(128 * WN, 1) void gemm_wgrad_group_kernel(WgGroup g
   const int nk = (kend - kbeg + BK - 1) / BK;
   const int ktail = kbeg + (nk - 1) * BK;
 
-  const __amdgpu_buffer_rsrc_t ra = make_rsrc(it.A);
-  const __amdgpu_buffer_rsrc_t rb = make_rsrc(it.B);
+  const u32x4 ra = rsrc4(it.A);
+  const u32x4 rb = rsrc4(it.B);
   typedef DmaPlan<BM, false, NW, MT> PA;
   typedef DmaPlan<BN, false, NW, MT> PB;
   PA pa;
