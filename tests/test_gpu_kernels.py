@@ -58,11 +58,12 @@ def test_linear_fwd_dgrad_wgrad(M, N, K, dtype):
     assert rel_err(gw.cpu(), 2 * (dyr.t() @ xr)) < tol
 
 
-@pytest.mark.parametrize("M,N,K", [(20000, 3000, 520), (9000, 2048, 40), (70000, 768, 136)])
+@pytest.mark.parametrize("M,N,K", [(20000, 3000, 520), (9000, 2048, 40), (70000, 768, 136), (25500, 768, 768)])
 def test_gemm_persistent_many_tiles(M, N, K):
     """More 256x256 tiles than CUs: each persistent workgroup walks several tiles, prefetching the
-    next tile's first K-tile during the epilogue (plain / activation+pre epilogues) or not
-    (residual epilogue), plus the fused column sums. fp32 torch matmul on the GPU as reference."""
+    next tile's first K-tile during the epilogue (plain kind) or not, plus the fused column sums
+    and the residual kind with dropout (exact keep pattern). fp32 torch matmul on the GPU as
+    reference."""
     o = ops()
     g = torch.Generator(device=DEV).manual_seed(M + K)
     x = torch.randn(M, K, device=DEV, generator=g).to(torch.bfloat16)
@@ -90,6 +91,14 @@ def test_gemm_persistent_many_tiles(M, N, K):
     yd = o.linear_fwd(xp, wp, act="relu", dropout=0.1, seed=77)
     keep = keep_mask(77, (M, N), 0.1).to(DEV)
     assert torch.equal(yd != 0, keep)
+    # the residual kind with dropout (out-proj / fc2 forward): drop(acc + b) + res
+    rz = torch.zeros(M, N, device=DEV, dtype=torch.bfloat16)
+    bp = b.abs() + 0.01
+    yr = o.linear_fwd(xp, wp, bp, res=rz, dropout=0.1, seed=78)
+    keep = keep_mask(78, (M, N), 0.1).to(DEV)
+    assert torch.equal(yr != 0, keep)
+    refp = (xp.float() @ wp.float().t() + bp) / 0.9
+    assert rel_err(torch.where(keep, yr.float(), refp), refp) < 1e-2
 
 
 @pytest.mark.parametrize("cfg", list(range(12)))
