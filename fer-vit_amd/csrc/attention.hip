@@ -1729,7 +1729,9 @@ extern "C" int fer_attention_fwd(int dtype, const void* qkv, int64_t ld_qkv, voi
   if (check_drop_range(drop_thresh, (long)B * H * N * (N + (N & 1)), "attention_fwd: dropout over >= 2^32 probabilities"))
     return -1;
   if (ld_qkv % 8 || ld_out % 4) return set_error("attention_fwd(bf16): misaligned leading dimension");
-  if ((long)B * N * ld_qkv * 2 >= 0x7FFFFFF0L) return set_error("attention_fwd(bf16): qkv exceeds 2 GiB");
+  // (the persistent kernel addresses qkv and out through 32-bit buffer offsets, bit 31 = out of range)
+  if ((long)B * N * ld_qkv * 2 >= 0x7FFFFFF0L || (long)B * N * ld_out * 2 >= 0x7FFFFFF0L)
+    return set_error("attention_fwd(bf16): qkv or out exceeds 2 GiB");
   const float sl2 = scale * LOG2E;
   if (N <= 256 && dh <= 64 && N > 224) {  // NB = 8: 9 waves would not fit 2/SIMD
     const int nb = (N + 31) / 32;
@@ -1811,7 +1813,7 @@ extern "C" int fer_attention_bwd(int dtype, const void* qkv, int64_t ld_qkv, con
     return -1;
   if (ld_qkv % 8 || ld_out % 8 || ld_dout % 8 || ld_dqkv % 8) return set_error("attention_bwd(bf16): misaligned ld");
   if ((long)B * N * ld_qkv * 2 >= 0x7FFFFFF0L || (long)B * N * ld_dout * 2 >= 0x7FFFFFF0L ||
-      (long)B * N * ld_dqkv * 2 >= 0x7FFFFFF0L)
+      (long)B * N * ld_dqkv * 2 >= 0x7FFFFFF0L || (long)B * N * ld_out * 2 >= 0x7FFFFFF0L)
     return set_error("attention_bwd(bf16): operand exceeds 2 GiB (buffer-resource range)");
   const int nb = (N + 31) / 32;
   const float sl2 = scale * LOG2E;

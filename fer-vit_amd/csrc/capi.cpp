@@ -1,4 +1,5 @@
 // C ABI glue: error state and the GEMM entry point.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -49,5 +50,24 @@ extern "C" int fer_set_step_counter(const uint64_t* counter) {
   if (fer::set_step_ptr_gemm(counter) || fer::set_step_ptr_attention(counter) ||
       fer::set_step_ptr_layernorm(counter) || fer::set_step_ptr_misc(counter))
     return fer::set_error("set_step_counter: hipMemcpyToSymbol failed");
+  return 0;
+}
+
+extern "C" int fer_stream_create_cu_mask(const uint32_t* mask, int nwords, int priority, fer_stream_t* out) {
+  if (!out || nwords < 0 || (nwords > 0 && !mask)) return fer::set_error("stream_create_cu_mask: bad arguments");
+  hipStream_t s = nullptr;
+  hipError_t e = nwords == 0 ? hipStreamCreateWithPriority(&s, hipStreamNonBlocking, priority)
+                             : hipExtStreamCreateWithCUMask(&s, (uint32_t)nwords, mask);
+  if (e != hipSuccess) {
+    char msg[160];
+    snprintf(msg, sizeof(msg), "stream_create_cu_mask: %s", hipGetErrorString(e));
+    return fer::set_error(msg);
+  }
+  *out = (fer_stream_t)s;
+  return 0;
+}
+
+extern "C" int fer_stream_destroy(fer_stream_t s) {
+  if (s && hipStreamDestroy((hipStream_t)s) != hipSuccess) return fer::set_error("stream_destroy failed");
   return 0;
 }

@@ -1144,8 +1144,6 @@ static int launch_pp(GemmArgs g, const EpiArgs& e, hipStream_t st) {
       case EPI_STORE: FER_PPK(EPI_STORE); break;
       case EPI_GATE: FER_PPK(EPI_GATE); break;
       case EPI_GATER: FER_PPK(EPI_GATER); break;
-      case EPI_RES: FER_PPK(EPI_RES); break;
-      case EPI_MUL: FER_PPK(EPI_MUL); break;
       case EPI_RES2: FER_PPK(EPI_RES2); break;
       case EPI_MUL2: FER_PPK(EPI_MUL2); break;
       default: FER_PPK(EPI_GEN); break;
@@ -1725,7 +1723,7 @@ FER_DEV int tile_8ph_pp(const GemmArgs& g, const PpEpi& e, int bid, char* smem, 
 // DYN: tiles from the per-stream work queue (common.h wq_*; the class of tile bid is bid & 7, the
 // XCD tile_of's remap gives it): the first tile is blockIdx.x, each tile claims the next one at
 // its start (tile_8ph claim_slot) and hands it on through LDS at its end. !DYN: fixed stride
-// (split-K launches, stream capture, FERVIT_FIXED_STRIDE).
+// (split-K launches, stream capture, fer_set_persistent_mode).
 template <bool AKC, bool BKC, int MT, bool DYN, int EK>
 __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmArgs g, EpiArgs e) {
   __shared__ __attribute__((aligned(1024))) char smem[8 * 16384 + 16];
@@ -2056,8 +2054,6 @@ static int launch_8ph(GemmArgs g, const EpiArgs& e, hipStream_t st) {
       case EPI_STORE: FER_8PH(DY, EPI_STORE); break;   \
       case EPI_GATE: FER_8PH(DY, EPI_GATE); break;     \
       case EPI_GATER: FER_8PH(DY, EPI_GATER); break;   \
-      case EPI_RES: FER_8PH(DY, EPI_RES); break;       \
-      case EPI_MUL: FER_8PH(DY, EPI_MUL); break;       \
       case EPI_RES2: FER_8PH(DY, EPI_RES2); break;     \
       case EPI_MUL2: FER_8PH(DY, EPI_MUL2); break;     \
       default: FER_8PH(DY, EPI_GEN); break;            \

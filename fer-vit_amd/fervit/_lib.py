@@ -53,6 +53,8 @@ SIGNATURES = {
     "fer_gemm": (i32, [C.POINTER(GemmDesc), C.POINTER(Epilogue), vp]),
     "fer_gemm_set_config": (i32, [i32]),
     "fer_set_persistent_mode": (i32, [i32]),
+    "fer_stream_create_cu_mask": (i32, [C.POINTER(C.c_uint32), i32, i32, C.POINTER(C.c_void_p)]),
+    "fer_stream_destroy": (i32, [vp]),
     "fer_gemm_colsum_ws": (i64, [i32, i32]),
     "fer_wgrad_group": (i32, [C.POINTER(WgradItem), i32, i32, fp, i64, vp]),
     "fer_wgrad_group_ws": (i64, [C.POINTER(WgradItem), i32, i32]),

@@ -118,9 +118,11 @@ class Reducer:
         if self.cuda:
             self.side.wait_stream(torch.cuda.current_stream(view.device))
             wg = runtime.WGRAD.stream(view.device)  # weight gradients finish on their own stream
-            # (under HIP-graph capture the weight gradients run on the capturing stream: waiting on
-            # the eager-only weight-gradient stream there would join uncaptured work)
-            if wg is not None and not torch.cuda.is_current_stream_capturing():
+            # Wait on it whenever the weight gradients actually run there: eagerly, and under
+            # HIP-graph capture with WGRAD.in_capture (the side stream is then a forked branch of
+            # the captured graph). With the stream off (capture without in_capture, or disabled)
+            # they ran on the compute stream, which self.side already waited for above.
+            if wg is not None and not runtime.WGRAD._off():
                 self.side.wait_stream(wg)
             with torch.cuda.stream(self.side):
                 b.work = self._allreduce(self._to_wire(b, view))

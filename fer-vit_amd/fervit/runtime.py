@@ -247,6 +247,35 @@ class _WgradStream:
         self.join_queued = False
         self.enabled = True
         self.in_capture = False
+        # CU mask of the side stream (list of 32-bit words, bit i = CU i; None: every CU). Set before
+        # the first backward; the stream is created on first use (fer_stream_create_cu_mask).
+        self.cu_mask: Optional[List[int]] = None
+        self._handles = {}
+
+    def _make(self, dev):
+        if not self.cu_mask:
+            return torch.cuda.Stream(device=dev)
+        import ctypes
+
+        from ._lib import check, lib
+
+        words = (ctypes.c_uint32 * len(self.cu_mask))(*[int(w) & 0xFFFFFFFF for w in self.cu_mask])
+        h = ctypes.c_void_p()
+        with torch.cuda.device(dev):
+            check(lib().fer_stream_create_cu_mask(words, len(self.cu_mask), 0, ctypes.byref(h)), "wgrad stream")
+        self._handles[dev] = h.value
+        return torch.cuda.ExternalStream(h.value, device=dev)
+
+    def reset(self):
+        """Drop the side streams (e.g. after changing cu_mask); call with no backward in flight."""
+        if self.streams:
+            torch.cuda.synchronize()
+        self.streams = {}
+        from ._lib import lib
+
+        for h in self._handles.values():
+            lib().fer_stream_destroy(h)
+        self._handles = {}
 
     def _off(self) -> bool:
         return not self.enabled or (not self.in_capture and torch.cuda.is_current_stream_capturing())
@@ -261,7 +290,7 @@ class _WgradStream:
         main = torch.cuda.current_stream(dev)
         side = self.streams.get(dev)
         if side is None:
-            side = self.streams[dev] = torch.cuda.Stream(device=dev)
+            side = self.streams[dev] = self._make(dev)
         side.wait_stream(main)
         with torch.cuda.stream(side):
             out = fn()

@@ -107,6 +107,14 @@ int fer_gemm_set_config(int cfg);
  * start-up). Results are bit-identical between the modes. */
 int fer_set_persistent_mode(int mode);
 
+/* A HIP stream whose kernels run only on the CUs set in mask (nwords 32-bit words, bit i = CU i in
+ * the driver's CU numbering; hipExtStreamCreateWithCUMask), or with nwords = 0 an unmasked stream
+ * of the given priority. For the weight-gradient side stream of the backward
+ * (`train/train_image_vit.py:124` loss.backward(): this path's dgrad / wgrad split over streams);
+ * the caller owns the stream (fer_stream_destroy). */
+int fer_stream_create_cu_mask(const uint32_t* mask, int nwords, int priority, fer_stream_t* out);
+int fer_stream_destroy(fer_stream_t stream);
+
 /* LayerNorm forward over rows of x [M][D] (nn.LayerNorm, biased variance;
  * post-norm `nn.TransformerEncoderLayer` norm1/norm2, heads `image_vit.py:162-163`,
  * `latent_vit.py:33-36`, timm pre-norm eps 1e-6). gamma/beta are [gamma_rows][D]:

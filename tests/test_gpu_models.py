@@ -3,7 +3,7 @@
 fp32 parity path: logits within 1e-3 of the reference PyTorch-CPU forward (BASELINE
 north star), argmax identical, loss, and every parameter-gradient checksum.
 bf16 fast path: the same checks with per-case gates at 2x the errors measured on the GPU
-(tools/bf16_parity_measure.py, profiles/r04o_bf16_parity.json), argmax on samples whose
+(tests/bf16_parity_measure.py, profiles/r04o_bf16_parity.json), argmax on samples whose
 top-1/top-2 margin exceeds 0.2; and at the headline size (ViT-B/16, bs 256) bf16 logits against
 this library's fp32 parity path on identical weights and inputs.
 """

@@ -34,6 +34,21 @@ for s in $STEPS; do
         FERVIT_LIB=$GRAFT_REPO_ROOT/fer-vit_amd/fervit/libfervit_st.so timeout -k 10 120 python -u tools/gemm_stamps.py $c \
           2>&1 | grep -v amdgpu.ids | sed "s/^/[$c] /" | tee -a gpurun_out/${TAG}_gemm_stamps.txt | grep -E "epilogue|prologue|steady" || exit 1
       done ;;
+    cumask)  # which CUs / XCDs a CU-masked stream's workgroups land on
+      timeout -k 10 120 ./tools/micro/cumask_probe > gpurun_out/${TAG}_cumask_probe.txt 2>&1 \
+        || { tail -20 gpurun_out/${TAG}_cumask_probe.txt; exit 1; }
+      cat gpurun_out/${TAG}_cumask_probe.txt ;;
+    hybgate)  # bf16 errors of the hybrid / expression-aware tests (their BF16_GATES = 2x these)
+      timeout -k 10 300 python -u tests/bf16_parity_measure.py --hybrid > gpurun_out/${TAG}_bf16_parity_hybrid.json \
+        2> gpurun_out/${TAG}_bf16_parity_hybrid.err || { tail -20 gpurun_out/${TAG}_bf16_parity_hybrid.err; exit 1; }
+      cat gpurun_out/${TAG}_bf16_parity_hybrid.json ;;
+    ab)  # interleaved in-process step A/B of the variants in $AB (tools/step_ab.py)
+      timeout -k 10 ${AB_TIMEOUT:-600} python -u tools/step_ab.py ${AB_ARGS:-} $AB > gpurun_out/${TAG}_step_ab.txt 2>&1 \
+        || { tail -20 gpurun_out/${TAG}_step_ab.txt; exit 1; }
+      grep -A40 "rounds x" gpurun_out/${TAG}_step_ab.txt ;;
+    fault)  # round-4 fault diagnosis: ONE launch of the faulting build; must stay the last step of a call
+      AMD_LOG_LEVEL=1 timeout -k 10 120 python -u tools/fault/run_fault.py > gpurun_out/${TAG}_fault.txt 2>&1
+      echo "fault step rc=$?"; grep -v "^:3:" gpurun_out/${TAG}_fault.txt | tail -20; exit 0 ;;
     prof)
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof -o run -- \
         python3 bench.py --steps 10 --warmup 5 --no-cpu-baseline --no-traffic > gpurun_out/${TAG}_prof.json 2>&1 \

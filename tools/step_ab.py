@@ -1,0 +1,137 @@
+"""Interleaved step-time A/B of run-time variants in ONE process (cdna_hip_programming.md rule 24).
+
+    python tools/step_ab.py --config vit_base_224 --rounds 4 --steps 10 base wg:m8lt6 wg:lt192 ...
+
+The model (bench.py build) is built once; every round runs each variant for --steps timed train
+steps (after one untimed step) and records the mean step time; the table gives the median and min
+over rounds. Variants:
+  base           as shipped
+  wg:<pred>      weight-gradient side stream restricted to the CUs whose mask bit satisfies <pred>
+  cs:<pred>      the whole step issued on a CU-masked compute stream (weight gradients unmasked)
+  both:<p1>/<p2> compute stream on <p1>, weight-gradient stream on <p2>
+  wgoff          weight gradients on the compute stream
+<pred>: lt<N> (bit < N), ge<N> (bit >= N), m<K>lt<N> (bit % K < N), m<K>ge<N> (bit % K >= N).
+"""
+import argparse
+import ctypes
+import os
+import re
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "fer-vit_amd"))
+
+import torch  # noqa: E402
+
+
+def mask_words(pred: str, ncu: int):
+    m = re.fullmatch(r"(lt|ge)(\d+)", pred)
+    if m:
+        op, n = m.group(1), int(m.group(2))
+        f = (lambda i: i < n) if op == "lt" else (lambda i: i >= n)
+    else:
+        m = re.fullmatch(r"m(\d+)(lt|ge)(\d+)", pred)
+        if not m:
+            raise SystemExit(f"bad mask predicate {pred}")
+        k, op, n = int(m.group(1)), m.group(2), int(m.group(3))
+        f = (lambda i: i % k < n) if op == "lt" else (lambda i: i % k >= n)
+    words = [0] * ((ncu + 31) // 32)
+    for i in range(ncu):
+        if f(i):
+            words[i // 32] |= 1 << (i % 32)
+    return words
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="vit_base_224")
+    ap.add_argument("--rounds", type=int, default=4)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("variants", nargs="+")
+    a = ap.parse_args()
+
+    import bench
+    from fervit import runtime
+    from fervit._lib import check, lib
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+    torch.manual_seed(42)
+    model, opt, crit, B, shape, desc = bench.build(a.config, dev)
+    g = torch.Generator(device=dev).manual_seed(42)
+    x = torch.randn(B, *shape, device=dev, generator=g)
+    y = torch.randint(0, 7, (B,), device=dev, generator=g)
+
+    def step():
+        opt.zero_grad()
+        loss = crit(model(x), y)
+        loss.backward()
+        opt.step()
+        return loss
+
+    cstreams = {}
+
+    def compute_stream(pred):
+        if pred not in cstreams:
+            words = mask_words(pred, ncu)
+            arr = (ctypes.c_uint32 * len(words))(*words)
+            h = ctypes.c_void_p()
+            check(lib().fer_stream_create_cu_mask(arr, len(words), 0, ctypes.byref(h)), "compute stream")
+            cstreams[pred] = torch.cuda.ExternalStream(h.value, device=dev)
+        return cstreams[pred]
+
+    def setup(v):
+        runtime.WGRAD.reset()
+        runtime.WGRAD.cu_mask = None
+        runtime.WGRAD.enabled = True
+        cs = None
+        if v == "base":
+            pass
+        elif v == "wgoff":
+            runtime.WGRAD.enabled = False
+        elif v.startswith("wg:"):
+            runtime.WGRAD.cu_mask = mask_words(v[3:], ncu)
+        elif v.startswith("cs:"):
+            cs = compute_stream(v[3:])
+        elif v.startswith("both:"):
+            p1, p2 = v[5:].split("/")
+            cs = compute_stream(p1)
+            runtime.WGRAD.cu_mask = mask_words(p2, ncu)
+        else:
+            raise SystemExit(f"unknown variant {v}")
+        return cs
+
+    def timed(v, n):
+        cs = setup(v)
+        ctx = torch.cuda.stream(cs) if cs is not None else torch.cuda.stream(torch.cuda.current_stream(dev))
+        with ctx:
+            step()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(n):
+                loss = step()
+            torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / n * 1e3, loss.item()
+
+    for v in a.variants:
+        timed(v, a.warmup)
+    res = {v: [] for v in a.variants}
+    for r in range(a.rounds):
+        for v in a.variants:
+            ms, lv = timed(v, a.steps)
+            res[v].append(ms)
+            print(f"round {r} {v:24s} {ms:8.3f} ms  loss {lv:.4f}", flush=True)
+    print(f"\n{a.config}: {a.rounds} rounds x {a.steps} steps per variant (ms/step)")
+    for v in a.variants:
+        xs = res[v]
+        print(f"  {v:24s} median {statistics.median(xs):8.3f}  min {min(xs):8.3f}  max {max(xs):8.3f}")
+    runtime.WGRAD.reset()
+
+
+if __name__ == "__main__":
+    main()
