@@ -29,6 +29,12 @@ class FusedAdamW(torch.optim.Optimizer):
         self.clip_coef: Optional[torch.Tensor] = None  # device scalar, consumed by the next step
         self._step_counter: Optional[torch.Tensor] = None  # graph mode (freeze_for_graph)
         self._frozen = None
+        # eager mode: the segment table stays on the device between steps and the per-step bias-
+        # correction step comes from a device counter (step = table step + *counter, advanced by one
+        # stream-ordered launch per step) -- no per-step pinned allocation and H2D copy. Re-uploaded
+        # when the segment set or any hyper-parameter changes.
+        self.cache_table = True
+        self._eager = None  # (device table, nseg, maxn, signature, counter)
 
     def zero_grad(self, set_to_none: bool = True):
         """torch semantics, plus: a clip coefficient left by clip_grad_norm_ for a step that was
@@ -81,6 +87,7 @@ class FusedAdamW(torch.optim.Optimizer):
         return sd
 
     def load_state_dict(self, state_dict):
+        self._eager = None
         super().load_state_dict(state_dict)
         flat = self._bind()
         with torch.no_grad():
@@ -103,6 +110,7 @@ class FusedAdamW(torch.optim.Optimizer):
         change of a group's lr / weight_decay / betas / eps (an LR scheduler's step) is written
         into the same device table before the next replay (sync_graph_hparams)."""
         flat = self._bind()
+        self._eager = None
         segs, maxn = self._segments(flat, bump=False)
         self._frozen = (self._upload(segs, flat), len(segs), maxn)
         # group of every segment (same walk as _segments), to rebuild the table with new hparams
@@ -150,6 +158,7 @@ class FusedAdamW(torch.optim.Optimizer):
                             st["step"] = st["step"] + n
         self._frozen = None
         self._step_counter = None
+        self._eager = None
 
     def _segments(self, flat, bump: bool):
         segs = []
@@ -201,12 +210,24 @@ class FusedAdamW(torch.optim.Optimizer):
         segs, maxn = self._segments(flat, bump=True)
         if not segs:
             return loss
-        dev = self._upload(segs, flat)
+        counter = None
+        sig = tuple(s[:7] for s in segs)
+        e = self._eager
+        if self.cache_table and e is not None and e[3] == sig and flat.data.is_cuda:
+            # same segments and hyper-parameters as the resident table, every step bumped by one since
+            dev, counter = e[0], e[4]
+            check(lib().fer_step_advance(counter.data_ptr(), ops.stream()), "adamw step")
+        else:
+            dev = self._upload(segs, flat)
+            self._eager = None
+            if self.cache_table and flat.data.is_cuda:
+                counter = torch.zeros(1, dtype=torch.int64, device=flat.data.device)
+                self._eager = (dev, len(segs), maxn, sig, counter)
         self._segs_dev = dev
         half = flat.bf16()
         check(lib().fer_adamw(flat.data.data_ptr(), flat.grad.data_ptr(), self._m.data_ptr(), self._v.data_ptr(),
                               half.data_ptr(), dev.data_ptr(), len(segs), maxn, float(self.grad_scale),
-                              ops.ptr(self._take_clip()), None, ops.stream()), "adamw")
+                              ops.ptr(self._take_clip()), ops.ptr(counter), ops.stream()), "adamw")
         flat.mark_half_fresh()
         return loss
 

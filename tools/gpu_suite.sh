@@ -49,6 +49,13 @@ for s in $STEPS; do
     fault)  # round-4 fault diagnosis: ONE launch of the faulting build; must stay the last step of a call
       AMD_LOG_LEVEL=1 timeout -k 10 120 python -u tools/fault/run_fault.py > gpurun_out/${TAG}_fault.txt 2>&1
       echo "fault step rc=$?"; grep -v "^:3:" gpurun_out/${TAG}_fault.txt | tail -20; exit 0 ;;
+    htrace)  # kernel + HIP API trace of a short bench run: compute-queue gaps vs host API calls
+      timeout -k 10 300 rocprofv3 --kernel-trace --hip-trace -d gpurun_out/${TAG}_htrace -o run -- \
+        python3 bench.py --steps 10 --warmup 5 --no-cpu-baseline --no-traffic --probe-steps 1 > gpurun_out/${TAG}_htrace.json 2>&1 \
+        || { tail -20 gpurun_out/${TAG}_htrace.json; exit 1; }
+      d=$(dirname $(find gpurun_out/${TAG}_htrace -name "*kernel_trace.csv" | head -1))
+      python3 tools/host_gaps.py "$d" 3 > gpurun_out/${TAG}_host_gaps.txt 2>&1 || true
+      head -40 gpurun_out/${TAG}_host_gaps.txt ;;
     prof)
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof -o run -- \
         python3 bench.py --steps 10 --warmup 5 --no-cpu-baseline --no-traffic > gpurun_out/${TAG}_prof.json 2>&1 \
