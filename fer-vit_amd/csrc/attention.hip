@@ -516,6 +516,139 @@ __global__ __launch_bounds__(64 * (NB + 1)) void attn_fwd_pers(const bf16* __res
   }
 }
 
+// ---------------------------------------------------------------- forward, occupancy form
+// The persistent forward's per-block arithmetic (lazy rescale, tree row sums, keep bits stored for
+// the backward) in one workgroup per (batch, head) of NB compute waves and no producer: <= 128
+// VGPRs and one K + V image (NB x 8 KB) per workgroup, so two workgroups share a CU (14 waves for
+// NB = 7: 3-4 per SIMD instead of the persistent kernel's 2). The persistent kernel hides the K / V
+// load behind the previous unit with a producer wave and a double buffer; here the other
+// workgroup's compute covers it, and the extra waves per SIMD hide the softmax / hashing VALU
+// latency (2 waves per SIMD issue at ~2.5 cycles per VALU instruction, 4 at ~1.2:
+// tools/micro/issue_rate.hip).
+template <int NB>
+__global__ __launch_bounds__(64 * NB) __attribute__((amdgpu_waves_per_eu(4))) void attn_fwd_occ(
+    const bf16* __restrict__ qkv, long ldq, bf16* __restrict__ out, long ldo, float* __restrict__ lse,
+    uint32_t* __restrict__ mask, int N, int H, int dh, float sl2, uint32_t thr, float dscale, uint64_t seed) {
+  constexpr int IMG = NB * 32 * 128;
+  __shared__ __attribute__((aligned(1024))) char lds[2 * IMG];
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), hh = lane >> 5;
+  const int bh = blockIdx.x, b = bh / H, h = bh - b * H, D = H * dh;
+  const int q = w * 32 + (lane & 31);
+  seed = step_seed(seed);  // (its load and wait ahead of the DMA: a wait after it would cover the DMA)
+  const u32x4 rs = rsrc4(qkv);
+  img_dma_asm<NB>(lds, rs, (long)b * N, ldq, D + h * dh, N, dh, w, lane);
+  img_dma_asm<NB>(lds + IMG, rs, (long)b * N, ldq, 2 * D + h * dh, N, dh, w, lane);
+  const __amdgpu_buffer_rsrc_t rq = make_rsrc(qkv), ro = make_rsrc(out), rl = make_rsrc(lse),
+                               rmk = make_rsrc(mask ? (const void*)mask : (const void*)lse);
+  bf16x8 qf[4];
+  {
+    const int so = __builtin_amdgcn_readfirstlane((int)((((long)b * N) * ldq + h * dh) * 2));
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int d0 = 16 * s + 8 * hh;
+      const uint32_t off = (((uint32_t)q * (uint32_t)ldq + (uint32_t)d0) * 2u) | ((uint32_t)(q >= N || d0 >= dh) << 31);
+      qf[s] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rq, off, so, 0));
+    }
+  }
+  wait_vm<0>();  // this wave's K / V pieces and its Q rows
+  asm volatile("" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3]));
+  bar_lds();  // every wave's pieces landed
+  const char* Ki = lds;
+  const char* Vi = lds + IMG;
+  const uint32_t row = drop_row(bh, N, q);
+  const uint32_t mk_off = (mask && lane < 32) ? (uint32_t)(lane * 4) : FER_OOB;
+  float m = -INFINITY, l = 0.f;
+  f32x16 ot[2] = {f32x16{}, f32x16{}};
+  bf16x8 kfr[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) kfr[s] = rd_row(Ki, lane & 31, 2 * s + hh);
+#pragma unroll 1
+  for (int kb = 0; kb < NB; ++kb) {
+    bf16x8 vfr[2][2];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int db = 0; db < 2; ++db) vfr[s2][db] = rd_tr(Vi, kb * 32 + 16 * s2, db * 32, lane);
+    f32x16 st = {};
+#pragma unroll
+    for (int s = 0; s < 4; ++s) st = mfma32(kfr[s], qf[s], st);
+    if (kb + 1 < NB) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) kfr[s] = rd_row(Ki, (kb + 1) * 32 + (lane & 31), 2 * s + hh);
+    }
+    if (kb == NB - 1 && NB * 32 > N) {  // only the last key block has padding keys
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        if (kb * 32 + acc_row(r, hh) >= N) st[r] = -INFINITY;
+    }
+    float bm = fmaxf(fmaxf(st[0], st[1]), st[2]);
+#pragma unroll
+    for (int r = 3; r < 15; r += 2) bm = fmaxf(fmaxf(bm, st[r]), st[r + 1]);
+    bm = fmaxf(bm, st[15]);
+    bm = xhalf_max(bm) * sl2;
+    if (__builtin_amdgcn_ballot_w64(bm > m + 8.f)) {  // lazy rescale (wave-uniform), as attn_fwd_pers
+      const float mn = fmaxf(m, bm);
+      const float al = ex2(m - mn);
+      m = mn;
+      l *= al;
+      ot[0] *= al;
+      ot[1] *= al;
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) st[r] = ex2(fmaf(st[r], sl2, -m));
+    float ls[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) ls[c] = (st[c] + st[c + 4]) + (st[c + 8] + st[c + 12]);
+    l += (ls[0] + ls[1]) + (ls[2] + ls[3]);
+    if (thr) {
+      const uint32_t p0 = (row >> 1) + kb * 16 + 2 * hh;
+      // two rounds of 8 ballots (16 SGPRs live instead of 32: the 16-ballot form spilled at 128 VGPRs)
+      uint32_t word = 0u;
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        uint64_t bal[8];
+#pragma unroll
+        for (int r = 0; r < 8; r += 2) {
+          const int rr = 8 * half + r;
+          const uint32_t hv = fer_hash(seed, p0 + (uint32_t)(acc_row(rr, 0) >> 1));
+          const bool k0 = (hv & 0xFFFFu) >= thr, k1 = (hv >> 16) >= thr;
+          st[rr] = k0 ? st[rr] : 0.f;
+          st[rr + 1] = k1 ? st[rr + 1] : 0.f;
+          bal[r] = __builtin_amdgcn_ballot_w64(k0);
+          bal[r + 1] = __builtin_amdgcn_ballot_w64(k1);
+        }
+        if (mask) word |= half ? wl_keys8<8>(0u, bal) : wl_keys8<0>(0u, bal);
+      }
+      if (mask) {
+        __builtin_amdgcn_raw_buffer_store_b32(word, rmk, mk_off,
+                                              __builtin_amdgcn_readfirstlane((int)((((long)bh * NB + kb) * NB + w) * 128)), 0);
+      }
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const bf16x8 pf = pack8(st, s2);
+#pragma unroll
+      for (int db = 0; db < 2; ++db) ot[db] = mfma32(vfr[s2][db], pf, ot[db]);
+    }
+  }
+  l = xhalf_sum(l);
+  const float mul = dscale / l;
+  const int so = __builtin_amdgcn_readfirstlane((int)((((long)b * N) * ldo + h * dh) * 2));
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const f32x16& a = ot[i >> 2];
+    const int g4 = i & 3;
+    const int d = (i >> 2) * 32 + 8 * g4 + 4 * hh;
+    const uint32_t off = (((uint32_t)q * (uint32_t)ldo + (uint32_t)d) * 2u) | ((uint32_t)(q >= N || d >= dh) << 31);
+    const bf16x4 v = {(bf16)(a[4 * g4] * mul), (bf16)(a[4 * g4 + 1] * mul), (bf16)(a[4 * g4 + 2] * mul),
+                      (bf16)(a[4 * g4 + 3] * mul)};
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), ro, off, so, 0);
+  }
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint((m + log2f(l)) * LN2), rl,
+                                        (q < N && hh == 0) ? (uint32_t)(q * 4) : FER_OOB,
+                                        __builtin_amdgcn_readfirstlane(bh * N * 4), 0);
+}
+
 // ---------------------------------------------------------------- backward, fused
 // One workgroup per (batch, head), NB waves, wave w owns key block w (K, V fragments in
 // registers, dK / dV accumulators). At step i wave w visits query block qb = (w + i) % NB, so
@@ -1678,6 +1811,8 @@ extern "C" int64_t fer_attention_ws(int dtype, int B, int N, int H) {
 }
 
 static bool pers_path(int dtype, int N, int dh) { return dtype == FER_BF16 && N <= 224 && dh <= 64; }
+// forward kernel for N <= 224, dh <= 64 (fer_attention_set_fwd_kernel): 1 persistent, 2 occupancy form
+static int g_fwd_kernel = 1;
 static int64_t lse_floats(int B, int N, int H) { return ((int64_t)B * H * N + 63) / 64 * 64; }
 // persistent kernels walk a fixed blockIdx stride instead of the work queue (fer_set_persistent_mode)
 static bool fixed_stride() { return fixed_stride_mode(); }
@@ -1738,6 +1873,19 @@ extern "C" int fer_attention_fwd(int dtype, const void* qkv, int64_t ld_qkv, voi
     FER_NB_SWITCH(nb, hipLaunchKernelGGL(attn_fwd_bf16<NB_>, dim3(B * H), dim3(64 * NB_), 0, st, (const bf16*)qkv,
                                          (long)ld_qkv, (bf16*)out, (long)ld_out, lse, N, H, dh, sl2, drop_thresh,
                                          drop_scale, seed));
+  } else if (N <= 224 && dh <= 64 && g_fwd_kernel == 2) {
+    const int nb = (N + 31) / 32;
+    uint32_t* mask = (drop_thresh && pers_path(dtype, N, dh)) ? (uint32_t*)(lse + lse_floats(B, N, H)) : nullptr;
+#define FER_FOCC2(NBV)                                                                                     \
+  case NBV:                                                                                                \
+    hipLaunchKernelGGL((attn_fwd_occ<NBV>), dim3(B * H), dim3(64 * NBV), 0, st, (const bf16*)qkv,          \
+                       (long)ld_qkv, (bf16*)out, (long)ld_out, lse, mask, N, H, dh, sl2, drop_thresh,       \
+                       drop_scale, seed);                                                                  \
+    break;
+    switch (nb) {
+      FER_FOCC2(1) FER_FOCC2(2) FER_FOCC2(3) FER_FOCC2(4) FER_FOCC2(5) FER_FOCC2(6) FER_FOCC2(7)
+    }
+#undef FER_FOCC2
   } else if (N <= 224 && dh <= 64) {
     const int nb = (N + 31) / 32;
     uint32_t* mask = (drop_thresh && pers_path(dtype, N, dh)) ? (uint32_t*)(lse + lse_floats(B, N, H)) : nullptr;
@@ -1883,4 +2031,10 @@ extern "C" int fer_attention_bwd(int dtype, const void* qkv, int64_t ld_qkv, con
   int rc = hip_check("attention_bwd_bf16");
   if (rc || !colsum) return rc;
   return colsum_pass(ws, ws_bytes);
+}
+
+extern "C" int fer_attention_set_fwd_kernel(int k) {
+  if (k < 0 || k > 2) return fer::set_error("attention_set_fwd_kernel: 0 (default), 1 (persistent) or 2 (occupancy form)");
+  g_fwd_kernel = k == 0 ? 1 : k;
+  return 0;
 }

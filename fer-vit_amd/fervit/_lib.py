@@ -63,6 +63,7 @@ SIGNATURES = {
     "fer_layernorm_bwd": (i32, [i32, vp, i64, vp, i64, fp, fp, fp, i32, i32, vp, i64, vp, i64, vp, u32, f32, u64,
                                 fp, fp, fp, i32, fp, i64, i32, i32, vp]),
     "fer_attention_ws": (i64, [i32, i32, i32, i32]),
+    "fer_attention_set_fwd_kernel": (i32, [i32]),
     "fer_attention_saved_floats": (i64, [i32, i32, i32, i32, i32, u32]),
     "fer_attention_fwd": (i32, [i32, vp, i64, vp, i64, fp, i64, i32, i32, i32, i32, f32, u32, f32, u64, fp, i64, vp]),
     "fer_attention_bwd": (i32, [i32, vp, i64, vp, i64, vp, i64, fp, i64, vp, i64, fp, i64, i32, i32, i32, i32, f32, u32,

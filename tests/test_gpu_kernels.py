@@ -653,3 +653,45 @@ def test_persistent_work_queue_streams_and_capture():
         assert torch.equal(o.linear_fwd(x, w), ref)
         torch.cuda.synchronize()
         assert torch.equal(cap_out, ref)
+
+
+@pytest.mark.parametrize("N,H,dh,B", [(197, 12, 64, 64), (19, 8, 64, 256), (37, 12, 64, 48), (10, 6, 64, 64),
+                                      (100, 4, 32, 16)])
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_attention_fwd_occupancy_form_bit_exact(N, H, dh, B, p):
+    """The occupancy form of the forward (fer_attention_set_fwd_kernel(2): one workgroup per (batch,
+    head), two per CU) runs the persistent kernel's arithmetic in the same order: output, lse and the
+    stored keep bits must agree bit for bit with it (fer_attention_set_fwd_kernel(1)), and the backward
+    fed from either gives identical gradients."""
+    from fervit._lib import lib
+
+    o = ops()
+    D = H * dh
+    g = torch.Generator(device=DEV).manual_seed(B * N + H + int(p * 10))
+    qkv = torch.randn(B * N, 3 * D, device=DEV, generator=g).to(torch.bfloat16)
+    dout = torch.randn(B * N, D, device=DEV, generator=g).to(torch.bfloat16)
+    res = []
+    try:
+        for k in (1, 2):
+            assert lib().fer_attention_set_fwd_kernel(k) == 0
+            out = torch.full((B * N, D), float("nan"), device=DEV, dtype=torch.bfloat16)
+            saved = o.attention_saved(qkv, B, N, H, dh, dropout=p)
+            saved.fill_(float("nan"))
+            o.attention_fwd(qkv, out, saved, B, N, H, dh, dropout=p, seed=99 + N)
+            dqkv = torch.empty_like(qkv)
+            o.attention_bwd(qkv, out, dout, saved, dqkv, B, N, H, dh, dropout=p, seed=99 + N)
+            torch.cuda.synchronize()
+            res.append((out, saved[:B * H * N].clone(), saved[B * H * N:].clone(), dqkv))
+    finally:
+        lib().fer_attention_set_fwd_kernel(0)
+    (o1, l1, m1, d1), (o2, l2, m2, d2) = res
+    assert torch.isfinite(o1.float()).all()
+    assert torch.equal(o1.view(torch.int16), o2.view(torch.int16))
+    assert torch.equal(l1.view(torch.int32), l2.view(torch.int32))
+    if p > 0:  # keep-bit words (the padding words after lse are never written by either kernel)
+        nb = (N + 31) // 32
+        off = (B * H * N + 63) // 64 * 64 - B * H * N
+        w1 = m1[off:off + B * H * nb * nb * 32].view(torch.int32)
+        w2 = m2[off:off + B * H * nb * nb * 32].view(torch.int32)
+        assert torch.equal(w1, w2)
+    assert torch.equal(d1.view(torch.int16), d2.view(torch.int16))

@@ -10,6 +10,7 @@ over rounds. Variants:
   cs:<pred>      the whole step issued on a CU-masked compute stream (weight gradients unmasked)
   both:<p1>/<p2> compute stream on <p1>, weight-gradient stream on <p2>
   wgoff          weight gradients on the compute stream
+  lib:<k>=<v>    a library selector for the variant: attnfwd (fer_attention_set_fwd_kernel), gemmcfg
 <pred>: lt<N> (bit < N), ge<N> (bit >= N), m<K>lt<N> (bit % K < N), m<K>ge<N> (bit % K >= N).
 """
 import argparse
@@ -86,6 +87,8 @@ def main():
         return cstreams[pred]
 
     def setup(v):
+        lib().fer_attention_set_fwd_kernel(0)
+        lib().fer_gemm_set_config(-1)
         runtime.WGRAD.reset()
         runtime.WGRAD.cu_mask = None
         runtime.WGRAD.enabled = True
@@ -94,6 +97,10 @@ def main():
             pass
         elif v == "wgoff":
             runtime.WGRAD.enabled = False
+        elif v.startswith("lib:"):  # a library run-time selector, e.g. lib:attnfwd=2
+            k, val = v[4:].split("=")
+            fn = {"attnfwd": "fer_attention_set_fwd_kernel", "gemmcfg": "fer_gemm_set_config"}[k]
+            check(getattr(lib(), fn)(int(val)), fn)
         elif v.startswith("wg:"):
             runtime.WGRAD.cu_mask = mask_words(v[3:], ncu)
         elif v.startswith("cs:"):
