@@ -1172,13 +1172,13 @@ static int launch_pp(GemmArgs g, const EpiArgs& e, hipStream_t st) {
 // (each >= 3 phases after its last read in the same buffer). Waits: q=3 retires A0/B0(T+1)
 // (vmcnt 6: A1, B1(T+1), A0(T+2) may fly), q=0 retires A1/B1(T) (vmcnt 4); a unit is read one
 // phase after the wait that retires it (the barrier between publishes other waves' DMA).
-template <bool KC, int MT, bool ISA>
+template <bool KC, int MT, bool ISA, int HR = 128>
 struct UnitPlan {
   uint32_t base[2];
   int kof[2];
   // local index (0..127) -> index inside the 256-wide tile
   FER_DEV static int map(int l, int q) {
-    return ISA ? (l >> 6) * 128 + q * 64 + (l & 63) : (l >> 5) * 64 + q * 32 + (l & 31);
+    return ISA ? (l >> 6) * HR + q * 64 + (l & 63) : (l >> 5) * 64 + q * 32 + (l & 31);
   }
   FER_DEV void init(int wave, int lane, long ld, int r0, int rmax, int q) {
 #pragma unroll
@@ -1250,7 +1250,7 @@ FER_DEV unsigned long long stamp_now() {
 // instruction -- measured 10-25 % slower kernels: profiles/r04k_gemm_ab.txt.)
 // MUL's fused column sums (cs_part): per lane over its rows, over the 8 row lanes of a column group,
 // then the two wave-row halves through LDS.
-template <int EK>
+template <int EK, int HR = 128>
 FER_DEV void tile_epilogue_wp(const GemmArgs& g, const EpiArgs& e, f32x4 (&acc)[4][8], char* smem, int m0, int n0,
                               int wr, int wc, int lane) {
   constexpr int S = epi_base(EK);
@@ -1281,12 +1281,12 @@ FER_DEV void tile_epilogue_wp(const GemmArgs& g, const EpiArgs& e, f32x4 (&acc)[
   const __amdgpu_buffer_rsrc_t rx = make_rsrc(X && xs ? xs : e.c);
   const uint32_t ldcb = (uint32_t)e.ldc * 2, ldpb = (uint32_t)e.ldp * 2;
   const uint32_t ldxb = X ? (uint32_t)(e.res ? e.ldr : e.ldx) * 2 : 0u;
-  const int rw0 = m0 + wr * 128 + prow;  // this lane's row in pass 0 of chunk 0
+  const int rw0 = m0 + wr * HR + prow;  // this lane's row in pass 0 of chunk 0
   auto load_x = [&](int c, bf16x8 (&xc)[4]) {
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
       const int row = rw0 + c * 32 + p * 8;
-      const uint32_t off = (nok && row < g.M) ? (uint32_t)row * ldxb + (uint32_t)n * 2 : FER_OOB;
+      const uint32_t off = (nok && row < g.M && (HR == 128 || c * 32 + p * 8 + prow < HR)) ? (uint32_t)row * ldxb + (uint32_t)n * 2 : FER_OOB;
       xc[p] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rx, off, 0, 0));
     }
   };
@@ -1311,7 +1311,7 @@ FER_DEV void tile_epilogue_wp(const GemmArgs& g, const EpiArgs& e, f32x4 (&acc)[
       const int lrow = p * 8 + prow;
       f32x4 v0 = *(const f32x4*)(buf + swz(lrow, pc >> 2)), v1 = *(const f32x4*)(buf + swz(lrow, (pc >> 2) + 1));
       const int row = rw0 + c * 32 + p * 8;
-      const bool ok = nok && row < g.M;
+      const bool ok = nok && row < g.M && (HR == 128 || c * 32 + p * 8 + prow < HR);  // (HR < 128: the half's rows end at HR)
       const uint32_t di = (uint32_t)row * (uint32_t)e.drop_ld + (uint32_t)n;
       epi8_kb<EK>(e, ok ? (uint32_t)row * ldcb + (uint32_t)n * 2 : FER_OOB,
                   ok ? (uint32_t)row * ldpb + (uint32_t)n * 2 : FER_OOB, di, v0, v1, b0, b1,
@@ -1349,7 +1349,11 @@ FER_DEV void tile_epilogue_wp(const GemmArgs& g, const EpiArgs& e, f32x4 (&acc)[
 // claim_slot (work-queue mode): thread 0 claims a tile at the start of this one, before the
 // prologue's operand DMA, and parks the id in that LDS word after the prologue's wait (which
 // retires the atomic together with the previous tile's epilogue stores and the first K-tile)
-template <bool AKC, bool BKC, int MT, int EK>
+// HR: rows per wave-row half. 128 = the 256-row tile; 112 = a 224-row tile (N = 768 linears: 678 tiles = 2.65
+// rounds of 256 CUs instead of 591 = 2.31), whose A units still load 128 rows per half (the 16 rows past
+// the half are the other half's / the next tile's, read but never used) and whose quadrant-row 1 skips its
+// last 16-row MFMA block.
+template <bool AKC, bool BKC, int MT, int EK, int HR = 128>
 FER_DEV void tile_8ph(const GemmArgs& g, const EpiArgs& e, int bid, char* smem, lds_vint* claim_slot) {
   typedef typename Acc<MT>::T AccT;
   constexpr int UNIT = 16384, BUF = 4 * UNIT;  // A0 A1 B0 B1
@@ -1374,7 +1378,7 @@ FER_DEV void tile_8ph(const GemmArgs& g, const EpiArgs& e, int bid, char* smem, 
   // GELU-gate fc1 forward: row groups of 4 tiles (377 -> 367-370 us alone, profiles/r03w_tile_group_ab.txt;
   // the other kinds gain nothing from it)
   tile_of(bid, g.tiles_m, g.tiles_n, tm, tn, EK == EPI_GATE ? 4 : 8);
-  const int m0 = tm * 256, n0 = tn * 256;
+  const int m0 = tm * (2 * HR), n0 = tn * 256;
   const int ks = blockIdx.y;
   const int kbeg = ks * g.k_chunk;
   const int kend = min(g.K, kbeg + g.k_chunk);
@@ -1383,7 +1387,7 @@ FER_DEV void tile_8ph(const GemmArgs& g, const EpiArgs& e, int bid, char* smem, 
 
   const __amdgpu_buffer_rsrc_t ra = make_rsrc(g.A);
   const __amdgpu_buffer_rsrc_t rb = make_rsrc(g.B);
-  UnitPlan<AKC, MT, true> pa0, pa1;
+  UnitPlan<AKC, MT, true, HR> pa0, pa1;
   UnitPlan<BKC, MT, false> pb0, pb1;
   pa0.init(wave, lane, g.lda, m0, g.M, 0);
   pa1.init(wave, lane, g.lda, m0, g.M, 1);
@@ -1464,7 +1468,8 @@ FER_DEV void tile_8ph(const GemmArgs& g, const EpiArgs& e, int bid, char* smem, 
         for (int j = 0; j < QJ; ++j)
 #pragma unroll
           for (int i = 0; i < QI; ++i)
-            acc[qn * QI + i][qm * QJ + j] = mfma<MT>(fb[qn][kk][i], fa[qm][kk][j], acc[qn * QI + i][qm * QJ + j]);
+            if (qm * QJ * MT + (j + 1) * MT <= HR)  // (HR < 128: the half's last rows carry no MFMA)
+              acc[qn * QI + i][qm * QJ + j] = mfma<MT>(fb[qn][kk][i], fa[qm][kk][j], acc[qn * QI + i][qm * QJ + j]);
       __builtin_amdgcn_s_setprio(0);
       __builtin_amdgcn_sched_barrier(0);
       if (T < 16) FER_STAMP(st_i + 3);
@@ -1475,8 +1480,10 @@ FER_DEV void tile_8ph(const GemmArgs& g, const EpiArgs& e, int bid, char* smem, 
   if (nk > 0 && !wr) __builtin_amdgcn_s_barrier();  // waves 0-3 catch up with the stagger
   FER_STAMP(2);
   static_assert(64 * (256 + 4) * 4 <= 2 * BUF, "epilogue staging (2 chunks per half) must fit");
+  static_assert(HR == 128 || (EK != EPI_GEN && MT == 16 && epi_base(EK) != EPI_MUL),
+                "224-row tiles: wave-private epilogue kinds without column sums only");
   if constexpr (EK != EPI_GEN && MT == 16)
-    tile_epilogue_wp<EK>(g, e, acc, smem, m0, n0, wr, wc, lane);
+    tile_epilogue_wp<EK, HR>(g, e, acc, smem, m0, n0, wr, wc, lane);
   else
     tile_epilogue<256, 256, 2, 4, MT, 2, 2 * BUF, EK>(g, e, acc, smem, m0, n0, ks, wr, wc, lane);
   FER_STAMP(3);
@@ -1724,7 +1731,7 @@ FER_DEV int tile_8ph_pp(const GemmArgs& g, const PpEpi& e, int bid, char* smem, 
 // XCD tile_of's remap gives it): the first tile is blockIdx.x, each tile claims the next one at
 // its start (tile_8ph claim_slot) and hands it on through LDS at its end. !DYN: fixed stride
 // (split-K launches, stream capture, fer_set_persistent_mode).
-template <bool AKC, bool BKC, int MT, bool DYN, int EK>
+template <bool AKC, bool BKC, int MT, bool DYN, int EK, int HR = 128>
 __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmArgs g, EpiArgs e) {
   __shared__ __attribute__((aligned(1024))) char smem[8 * 16384 + 16];
   const int ntiles = g.tiles_m * g.tiles_n;
@@ -1744,7 +1751,7 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmArgs g, EpiArgs e)
   } else if constexpr (!DYN) {
 #pragma unroll 1
     for (int bid = blockIdx.x; bid < ntiles; bid += gridDim.x) {
-      tile_8ph<AKC, BKC, MT, EK>(g, e, bid, smem, nullptr);
+      tile_8ph<AKC, BKC, MT, EK, HR>(g, e, bid, smem, nullptr);
       bar_lds();  // every wave is done with the epilogue's LDS before the next tile's DMA
     }
   } else {
@@ -1752,7 +1759,7 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmArgs g, EpiArgs e)
     int bid = wq_first(ntiles), par = 0;
 #pragma unroll 1
     while (bid >= 0) {
-      tile_8ph<AKC, BKC, MT, EK>(g, e, bid, smem, slot + par);
+      tile_8ph<AKC, BKC, MT, EK, HR>(g, e, bid, smem, slot + par);
       bar_lds();  // every wave is done with the epilogue's LDS before the next tile's DMA
       bid = __builtin_amdgcn_readfirstlane(slot[par]);
       par ^= 1;
@@ -2023,9 +2030,15 @@ static int launch_ring(GemmArgs g, const EpiArgs& e, hipStream_t st) {
   return 0;
 }
 
+static int g_row_tile = 256;  // fer_gemm_set_row_tile
+
 template <bool AKC, bool BKC, int MT>
 static int launch_8ph(GemmArgs g, const EpiArgs& e, hipStream_t st) {
-  g.tiles_m = (g.M + 255) / 256;
+  // fixed-flag epilogues for the K-contiguous MT16 kernel (the forward and transposed-shadow dgrad path)
+  const int ek = (AKC && BKC && MT == 16 && !g.partial) ? epi_kind(e, g.M, g.N) : EPI_GEN;
+  // 224-row tiles (fer_gemm_set_row_tile) for the residual kind of the N <= 768 linears
+  const bool r224 = g_row_tile == 224 && ek == EPI_RES2 && g.N <= 768 && g.splits == 1;
+  g.tiles_m = r224 ? (g.M + 223) / 224 : (g.M + 255) / 256;
   g.tiles_n = (g.N + 255) / 256;
   static const int ncu = [] {
     int dev = 0, n = 0;
@@ -2045,8 +2058,6 @@ static int launch_8ph(GemmArgs g, const EpiArgs& e, hipStream_t st) {
     for (int c = 0; c < 8; ++c) g.tq_base[c] = w.base[c];
   }
   dim3 grid(gx, g.splits);
-  // fixed-flag epilogues for the K-contiguous MT16 kernel (the forward and transposed-shadow dgrad path)
-  const int ek = (AKC && BKC && MT == 16 && !g.partial) ? epi_kind(e, g.M, g.N) : EPI_GEN;
 #define FER_8PH(DY, K) hipLaunchKernelGGL((gemm_8ph_kernel<AKC, BKC, MT, DY, K>), grid, dim3(512), 0, st, g, e)
 #define FER_8PH_K(DY)                                  \
   if constexpr (AKC && BKC && MT == 16) {              \
@@ -2060,6 +2071,14 @@ static int launch_8ph(GemmArgs g, const EpiArgs& e, hipStream_t st) {
     }                                                  \
   } else {                                             \
     FER_8PH(DY, EPI_GEN);                              \
+  }
+  if constexpr (AKC && BKC && MT == 16) {
+    if (r224) {
+      if (g.tq) hipLaunchKernelGGL((gemm_8ph_kernel<AKC, BKC, MT, true, EPI_RES2, 112>), grid, dim3(512), 0, st, g, e);
+      else hipLaunchKernelGGL((gemm_8ph_kernel<AKC, BKC, MT, false, EPI_RES2, 112>), grid, dim3(512), 0, st, g, e);
+      wq_check_launch(st, w);
+      return 0;
+    }
   }
   if (g.tq) {
     FER_8PH_K(true)
@@ -2310,6 +2329,12 @@ int fer::set_step_ptr_gemm(const uint64_t* p) { return set_step_ptr_here(p) == h
 extern "C" int64_t fer_gemm_colsum_ws(int M, int N) {
   // tile partials (128-row tiles at most) or the stand-alone colsum pass's partials
   return (int64_t)std::max(fer::ceil_div(std::max(M, 1), 128), 256) * N * 4;
+}
+
+extern "C" int fer_gemm_set_row_tile(int rows) {
+  if (rows != 256 && rows != 224) return fer::set_error("gemm_set_row_tile: 256 or 224");
+  fer::g_row_tile = rows;
+  return 0;
 }
 
 extern "C" int fer_gemm_set_config(int cfg) {

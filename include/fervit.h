@@ -76,6 +76,10 @@ typedef struct {
 } fer_epilogue;
 
 int fer_gemm(const fer_gemm_desc* d, const fer_epilogue* e, fer_stream_t stream);
+/* Row height of the 8-phase kernel's tiles for the residual-epilogue linears with N <= 768 (ViT-B's
+ * out_proj / linear2 forward and linear1 / in_proj input gradients, `image_vit.py:101-113`): 256
+ * (default) or 224 (678 instead of 591 tiles at 50,432 rows: 2.65 instead of 2.31 rounds of 256 CUs). */
+int fer_gemm_set_row_tile(int rows);
 
 /* Grouped weight gradients: dw[n][k] (+)= sum_m dy[m][n] x[m][k] (bf16 dy [M][N] row stride ld_dy,
  * bf16 x [M][K] row stride ld_x, fp32 dw [N][K] row stride ld_dw) for up to 8 nn.Linear weights

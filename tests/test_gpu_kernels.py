@@ -695,3 +695,36 @@ def test_attention_fwd_occupancy_form_bit_exact(N, H, dh, B, p):
         w2 = m2[off:off + B * H * nb * nb * 32].view(torch.int32)
         assert torch.equal(w1, w2)
     assert torch.equal(d1.view(torch.int16), d2.view(torch.int16))
+
+
+@pytest.mark.parametrize("M,N,K", [(50432, 768, 768), (20000, 768, 3072), (1000, 768, 520), (4000, 512, 1024),
+                                   (333, 256, 64)])
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_gemm_row_tile_224_bit_exact(M, N, K, p):
+    """224-row tiles (fer_gemm_set_row_tile(224): the residual kind of the N <= 768 linears) against the
+    256-row tiles: every output element sums the same K in the same order, so the residual + bias +
+    dropout epilogue output must agree bit for bit; every row (including the 16 past each wave-row
+    half, whose A rows are loaded but carry no MFMA) written exactly once (NaN-prefilled output)."""
+    from fervit._lib import lib
+
+    o = ops()
+    g = torch.Generator(device=DEV).manual_seed(M + N + K)
+    x = torch.randn(M, K, device=DEV, generator=g).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV, generator=g) / math.sqrt(K)).to(torch.bfloat16)
+    b = torch.randn(N, device=DEV, generator=g)
+    res = torch.randn(M, N, device=DEV, generator=g).to(torch.bfloat16)
+    outs = []
+    try:
+        for rows in (256, 224):
+            assert lib().fer_gemm_set_row_tile(rows) == 0
+            y = torch.full((M, N), float("nan"), device=DEV, dtype=torch.bfloat16)
+            o.linear_fwd(x, w, b, out=y, res=res, dropout=p, seed=1234, drop_ld=N)
+            torch.cuda.synchronize()
+            outs.append(y)
+    finally:
+        lib().fer_gemm_set_row_tile(256)
+    assert torch.isfinite(outs[1].float()).all()
+    assert torch.equal(outs[0].view(torch.int16), outs[1].view(torch.int16))
+    if p == 0.0:
+        ref = x.float() @ w.float().t() + b + res.float()
+        assert rel_err(outs[1], ref) < 1e-2

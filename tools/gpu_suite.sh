@@ -56,6 +56,10 @@ for s in $STEPS; do
       d=$(dirname $(find gpurun_out/${TAG}_htrace -name "*kernel_trace.csv" | head -1))
       python3 tools/host_gaps.py "$d" 3 > gpurun_out/${TAG}_host_gaps.txt 2>&1 || true
       head -40 gpurun_out/${TAG}_host_gaps.txt ;;
+    fwdcc)  # two concurrent half-batch forwards vs sequential (tools/fwd_concurrency.py)
+      timeout -k 10 300 python -u tools/fwd_concurrency.py > gpurun_out/${TAG}_fwd_concurrency.txt 2>&1 \
+        || { tail -20 gpurun_out/${TAG}_fwd_concurrency.txt; exit 1; }
+      grep -v amdgpu.ids gpurun_out/${TAG}_fwd_concurrency.txt ;;
     prof)
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof -o run -- \
         python3 bench.py --steps 10 --warmup 5 --no-cpu-baseline --no-traffic > gpurun_out/${TAG}_prof.json 2>&1 \

@@ -10,7 +10,7 @@ over rounds. Variants:
   cs:<pred>      the whole step issued on a CU-masked compute stream (weight gradients unmasked)
   both:<p1>/<p2> compute stream on <p1>, weight-gradient stream on <p2>
   wgoff          weight gradients on the compute stream
-  lib:<k>=<v>    a library selector for the variant: attnfwd (fer_attention_set_fwd_kernel), gemmcfg
+  lib:<k>=<v>    a library selector for the variant: attnfwd (fer_attention_set_fwd_kernel), gemmcfg, rowtile
 <pred>: lt<N> (bit < N), ge<N> (bit >= N), m<K>lt<N> (bit % K < N), m<K>ge<N> (bit % K >= N).
 """
 import argparse
@@ -89,6 +89,7 @@ def main():
     def setup(v):
         lib().fer_attention_set_fwd_kernel(0)
         lib().fer_gemm_set_config(-1)
+        lib().fer_gemm_set_row_tile(256)
         runtime.WGRAD.reset()
         runtime.WGRAD.cu_mask = None
         runtime.WGRAD.enabled = True
@@ -99,7 +100,8 @@ def main():
             runtime.WGRAD.enabled = False
         elif v.startswith("lib:"):  # a library run-time selector, e.g. lib:attnfwd=2
             k, val = v[4:].split("=")
-            fn = {"attnfwd": "fer_attention_set_fwd_kernel", "gemmcfg": "fer_gemm_set_config"}[k]
+            fn = {"attnfwd": "fer_attention_set_fwd_kernel", "gemmcfg": "fer_gemm_set_config",
+                  "rowtile": "fer_gemm_set_row_tile"}[k]
             check(getattr(lib(), fn)(int(val)), fn)
         elif v.startswith("wg:"):
             runtime.WGRAD.cu_mask = mask_words(v[3:], ncu)
