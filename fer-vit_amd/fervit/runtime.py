@@ -124,12 +124,29 @@ class FlatParams:
         # (not the flat base's), so the signature is the sum over parameters.
         return self.data._version + sum(p._version for p in self.params)
 
-    def mark_half_fresh(self):
+    def mark_half_fresh(self, refresh: bool = True):
         """Called by the fused optimizer right after it rewrote the bf16 copy (same stream):
-        the transposed copies follow in the same stream order (and the same captured graph)."""
+        the transposed copies follow in the same stream order (and the same captured graph);
+        refresh=False when the optimizer refreshed them per parameter set already."""
         self.half_version = self.version()
         self._checked = True
-        self.refresh_half_t()
+        if refresh:
+            self.refresh_half_t()
+
+    def half_t_segments(self, params):
+        """(device segment table, tile count) of the transposed-copy refresh for the 2-D parameters in
+        `params` (None when there are none or no transposed copy exists yet)."""
+        if self.half_t is None:
+            return None, 0
+        segs, tiles = [], 0
+        for q in params:
+            if q.dim() == 2:
+                r, c = q.shape
+                segs.append((self.offsets[id(q)], r, c, tiles))
+                tiles += -(-r // 64) * -(-c // 64)
+        if not segs:
+            return None, 0
+        return torch.tensor(segs, dtype=torch.int64).to(self.device), tiles
 
     def half_view(self, p):
         return self.view(p, self.bf16())

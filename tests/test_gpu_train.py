@@ -300,3 +300,45 @@ def test_zero_grad_drops_a_pending_clip_coefficient():
     assert m._fer_clip_coef is not None
     o.zero_grad()  # the step is skipped
     assert m._fer_clip_coef is None and o.clip_coef is None
+
+
+@pytest.mark.parametrize("prec", ["bf16", "fp32"])
+def test_step_in_backward_equals_step(prec):
+    """FusedAdamW.step_in_backward (each layer's update issued from the backward's gradient-ready hook on
+    the weight-gradient stream) == the same optimizer's plain step() after the backward: parameters,
+    AdamW moments, the bf16 shadow and its transposed copies bit for bit over three dropout train steps
+    of an ImageViT (every parameter kind: patch embedding, CLS / pos, encoder layers, head)."""
+    import fervit
+    from fervit.loss import CrossEntropyLoss
+    from fervit.optim import FusedAdamW
+    from models_fer_vit.image_vit import ImageViT
+
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(16, 3, 48, 48, generator=g).to(DEV)
+    y = torch.randint(0, 7, (16,), generator=g).to(DEV)
+    crit = CrossEntropyLoss(label_smoothing=0.1)
+    out = []
+    for inbw in (False, True):
+        torch.manual_seed(0)
+        m = ImageViT(img_size=48, patch_size=16, embed_dim=384, depth=2, heads=8, mlp_dim=1536, dropout=0.1)
+        m = m.to(DEV).set_precision(prec)
+        opt = FusedAdamW(m.parameters(), lr=1e-3, weight_decay=0.05, model=m).step_in_backward(inbw)
+        fervit.manual_seed(11)
+        for _ in range(3):
+            opt.zero_grad()
+            crit(m(x), y).backward()
+            opt.step()
+        torch.cuda.synchronize()
+        flat = m.fer_flat()
+        out.append((flat.data.clone(), opt._m.clone(), opt._v.clone(),
+                    None if flat.half is None else flat.half.clone(),
+                    None if flat.half_t is None else flat.half_t.clone(),
+                    [opt.state[p]["step"] for p in m.parameters()]))
+        opt.step_in_backward(False)
+    a, b = out
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]) and torch.equal(a[2], b[2])
+    if a[3] is not None:
+        assert torch.equal(a[3].view(torch.int16), b[3].view(torch.int16))
+    if a[4] is not None:
+        assert torch.equal(a[4].view(torch.int16), b[4].view(torch.int16))
+    assert a[5] == b[5]

@@ -10,6 +10,7 @@ over rounds. Variants:
   cs:<pred>      the whole step issued on a CU-masked compute stream (weight gradients unmasked)
   both:<p1>/<p2> compute stream on <p1>, weight-gradient stream on <p2>
   wgoff          weight gradients on the compute stream
+  adamwbw        FusedAdamW.step_in_backward (per-layer updates from the backward's gradient-ready hook)
   lib:<k>=<v>    a library selector for the variant: attnfwd (fer_attention_set_fwd_kernel), gemmcfg, rowtile
 <pred>: lt<N> (bit < N), ge<N> (bit >= N), m<K>lt<N> (bit % K < N), m<K>ge<N> (bit % K >= N).
 """
@@ -90,6 +91,7 @@ def main():
         lib().fer_attention_set_fwd_kernel(0)
         lib().fer_gemm_set_config(-1)
         lib().fer_gemm_set_row_tile(256)
+        opt.step_in_backward(False)
         runtime.WGRAD.reset()
         runtime.WGRAD.cu_mask = None
         runtime.WGRAD.enabled = True
@@ -98,6 +100,8 @@ def main():
             pass
         elif v == "wgoff":
             runtime.WGRAD.enabled = False
+        elif v == "adamwbw":  # optimizer step inside the backward (FusedAdamW.step_in_backward)
+            opt.step_in_backward(True)
         elif v.startswith("lib:"):  # a library run-time selector, e.g. lib:attnfwd=2
             k, val = v[4:].split("=")
             fn = {"attnfwd": "fer_attention_set_fwd_kernel", "gemmcfg": "fer_gemm_set_config",
