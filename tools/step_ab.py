@@ -5,7 +5,8 @@
 The model (bench.py build) is built once; every round runs each variant for --steps timed train
 steps (after one untimed step) and records the mean step time; the table gives the median and min
 over rounds. Variants:
-  base           as shipped
+  base           as shipped (bench.py: the step on the legacy null stream)
+  nb:<variant>   the variant with the step on a non-blocking stream (every variant below does that)
   wg:<pred>      weight-gradient side stream restricted to the CUs whose mask bit satisfies <pred>
   cs:<pred>      the whole step issued on a CU-masked compute stream (weight gradients unmasked)
   both:<p1>/<p2> compute stream on <p1>, weight-gradient stream on <p2>
@@ -76,45 +77,58 @@ def main():
         opt.step()
         return loss
 
-    cstreams = {}
+    # Streams are created once per CU mask and never destroyed (the caching allocator keeps events of
+    # the streams its blocks were used on), and every variant after "base" issues its step on a
+    # non-blocking compute stream: hipExtStreamCreateWithCUMask streams are BLOCKING streams, which
+    # synchronise with the legacy null stream bench.py's step runs on.
+    streams = {}
 
-    def compute_stream(pred):
-        if pred not in cstreams:
+    def masked(pred):
+        if pred not in streams:
             words = mask_words(pred, ncu)
             arr = (ctypes.c_uint32 * len(words))(*words)
             h = ctypes.c_void_p()
-            check(lib().fer_stream_create_cu_mask(arr, len(words), 0, ctypes.byref(h)), "compute stream")
-            cstreams[pred] = torch.cuda.ExternalStream(h.value, device=dev)
-        return cstreams[pred]
+            check(lib().fer_stream_create_cu_mask(arr, len(words), 0, ctypes.byref(h)), "masked stream")
+            streams[pred] = torch.cuda.ExternalStream(h.value, device=dev)
+        return streams[pred]
+
+    nb_compute = torch.cuda.Stream(device=dev)
+    default_side = {}
 
     def setup(v):
         lib().fer_attention_set_fwd_kernel(0)
         lib().fer_gemm_set_config(-1)
         lib().fer_gemm_set_row_tile(256)
         opt.step_in_backward(False)
-        runtime.WGRAD.reset()
-        runtime.WGRAD.cu_mask = None
         runtime.WGRAD.enabled = True
-        cs = None
+        if "side" not in default_side:  # the shipped side stream (created by the first backward)
+            default_side["side"] = runtime.WGRAD.streams.get(dev)
+        runtime.WGRAD.streams[dev] = default_side["side"]
+        if runtime.WGRAD.streams[dev] is None:
+            del runtime.WGRAD.streams[dev]
         if v == "base":
+            return None
+        cs = nb_compute
+        body = v[3:] if v.startswith("nb:") else v
+        if body == "base":
             pass
-        elif v == "wgoff":
+        elif body == "wgoff":
             runtime.WGRAD.enabled = False
-        elif v == "adamwbw":  # optimizer step inside the backward (FusedAdamW.step_in_backward)
+        elif body == "adamwbw":  # optimizer step inside the backward (FusedAdamW.step_in_backward)
             opt.step_in_backward(True)
-        elif v.startswith("lib:"):  # a library run-time selector, e.g. lib:attnfwd=2
-            k, val = v[4:].split("=")
+        elif body.startswith("lib:"):  # a library run-time selector, e.g. lib:attnfwd=2
+            k, val = body[4:].split("=")
             fn = {"attnfwd": "fer_attention_set_fwd_kernel", "gemmcfg": "fer_gemm_set_config",
                   "rowtile": "fer_gemm_set_row_tile"}[k]
             check(getattr(lib(), fn)(int(val)), fn)
-        elif v.startswith("wg:"):
-            runtime.WGRAD.cu_mask = mask_words(v[3:], ncu)
-        elif v.startswith("cs:"):
-            cs = compute_stream(v[3:])
-        elif v.startswith("both:"):
-            p1, p2 = v[5:].split("/")
-            cs = compute_stream(p1)
-            runtime.WGRAD.cu_mask = mask_words(p2, ncu)
+        elif body.startswith("wg:"):
+            runtime.WGRAD.streams[dev] = masked(body[3:])
+        elif body.startswith("cs:"):
+            cs = masked(body[3:])
+        elif body.startswith("both:"):
+            p1, p2 = body[5:].split("/")
+            cs = masked(p1)
+            runtime.WGRAD.streams[dev] = masked(p2)
         else:
             raise SystemExit(f"unknown variant {v}")
         return cs
@@ -123,6 +137,8 @@ def main():
         cs = setup(v)
         ctx = torch.cuda.stream(cs) if cs is not None else torch.cuda.stream(torch.cuda.current_stream(dev))
         with ctx:
+            if cs is not None:
+                cs.wait_stream(torch.cuda.default_stream(dev))
             step()
             torch.cuda.synchronize()
             t0 = time.perf_counter()
@@ -143,7 +159,6 @@ def main():
     for v in a.variants:
         xs = res[v]
         print(f"  {v:24s} median {statistics.median(xs):8.3f}  min {min(xs):8.3f}  max {max(xs):8.3f}")
-    runtime.WGRAD.reset()
 
 
 if __name__ == "__main__":
