@@ -27,13 +27,22 @@ def main():
     fl_f = 4.0 * N * N * dh * B * H
     by_f = 2.0 * M * 4 * D
     by_b = 2.0 * M * 8 * D
-    for p in (0.1, 0.0):
-        lse = ops.attention_saved(qkv, B, N, H, dh, dropout=p)
-        tf = min(timeit(lambda: ops.attention_fwd(qkv, out, lse, B, N, H, dh, dropout=p, seed=5)) for _ in range(3))
-        tb = min(timeit(lambda: ops.attention_bwd(qkv, out, dout, lse, dqkv, B, N, H, dh, dropout=p, seed=5))
-                 for _ in range(3))
-        print(f"p={p}: fwd {tf * 1e3:7.1f} us ({fl_f / tf / 1e9:6.1f} TF, {by_f / tf / 1e6:5.2f} GB/s)   "
-              f"bwd {tb * 1e3:7.1f} us ({2 * fl_f / tb / 1e9:6.1f} TF, {by_b / tb / 1e6:5.2f} GB/s)", flush=True)
+    from fervit._lib import lib
+
+    # forward kernels (fer_attention_set_fwd_kernel: 1 persistent, 2 occupancy form), interleaved
+    for rep in range(2):
+        for p in (0.1, 0.0):
+            for fk in (1, 2):
+                lib().fer_attention_set_fwd_kernel(fk)
+                lse = ops.attention_saved(qkv, B, N, H, dh, dropout=p)
+                tf = min(timeit(lambda: ops.attention_fwd(qkv, out, lse, B, N, H, dh, dropout=p, seed=5))
+                         for _ in range(3))
+                tb = min(timeit(lambda: ops.attention_bwd(qkv, out, dout, lse, dqkv, B, N, H, dh, dropout=p, seed=5))
+                         for _ in range(3))
+                print(f"p={p} fwd kernel {fk}: fwd {tf * 1e3:7.1f} us ({fl_f / tf / 1e9:6.1f} TF, "
+                      f"{by_f / tf / 1e6:5.2f} GB/s)   bwd {tb * 1e3:7.1f} us ({2 * fl_f / tb / 1e9:6.1f} TF, "
+                      f"{by_b / tb / 1e6:5.2f} GB/s)", flush=True)
+    lib().fer_attention_set_fwd_kernel(0)
 
 
 if __name__ == "__main__":

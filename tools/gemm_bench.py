@@ -36,6 +36,8 @@ def main():
     pre = torch.empty(M, F, device=dev, dtype=torch.bfloat16)
     gw = torch.empty(F, D, device=dev)
     w2t, w1t = w2.t().contiguous(), w1.t().contiguous()  # [F, D], [D, F]
+    wo, bo = r(D, D) * 0.03, torch.zeros(D, device=dev)
+    q3, wqkvt = r(M, 3 * D), wqkv.t().contiguous()  # dqkv [M, 3D], W_qkv^T [D, 3D]
     out_f = torch.empty(M, F, device=dev, dtype=torch.bfloat16)
     out_d = torch.empty(M, D, device=dev, dtype=torch.bfloat16)
     cs = torch.zeros(F, device=dev)
@@ -62,6 +64,11 @@ def main():
         "fc1 dgrad +res (B MN, K=3072)": (lambda: ops.linear_dgrad(h, w1, out=out_d, res=x), 2 * M * F * D, None),
         "fc1 dgrad +res (B KC, K=3072)": (lambda: ops.linear_fwd(h, w1t, out=out_d, res=x), 2 * M * F * D, None),
         "fc1 wgrad (MN,MN splitK)": (lambda: ops.linear_wgrad(dF, x, gw), 2 * M * F * D, lambda: dF.t() @ x),
+        "out-proj fwd +bias+drop+res": (lambda: ops.linear_fwd(x, wo, bo, out=out_d, res=x, dropout=0.1, seed=3),
+                                        2 * M * D * D, None),
+        "fc2 fwd +bias+drop+res (K=3072)": (lambda: ops.linear_fwd(h, w2, bo, out=out_d, res=x, dropout=0.1, seed=3),
+                                            2 * M * F * D, None),
+        "qkv dgrad +res (B KC, K=2304)": (lambda: ops.linear_fwd(q3, wqkvt, out=out_d, res=x), 2 * M * 3 * D * D, None),
     }
     cfg = os.environ.get("GB_CFG")  # force one tile configuration (fer_gemm_set_config)
     if cfg is not None:
@@ -71,21 +78,33 @@ def main():
     only = os.environ.get("GB_ONLY")
     if only:
         cases = {k: v for k, v in cases.items() if only in k}
-    res = {k: [] for k in cases}
+    # GB_ROWS=ab: every case at both row tiles of fer_gemm_set_row_tile (256, 224), interleaved
+    rows = [256, 224] if os.environ.get("GB_ROWS") == "ab" else [None]
+    from fervit._lib import lib
+
+    res = {(k, rt): [] for k in cases for rt in rows}
     ref = {k: [] for k in cases}
     for _ in range(3):
         for k, (fn, fl, tf) in cases.items():
-            res[k].append(timeit(fn))
+            for rt in rows:
+                if rt is not None:
+                    lib().fer_gemm_set_row_tile(rt)
+                res[(k, rt)].append(timeit(fn))
             if tf is not None:
                 ref[k].append(timeit(tf))
+    if rows[0] is not None:
+        lib().fer_gemm_set_row_tile(256)
     tag = cfg if cfg is not None else "auto"
     for k, (fn, fl, tf) in cases.items():
-        t = min(res[k])
-        line = f"[cfg {tag}] {k:32s} ours {t * 1e3:8.1f} us  {fl / t / 1e9:7.1f} TF ({fl / t / 1e9 / PEAK * 100:4.1f}%)"
-        if ref[k]:
-            tr = min(ref[k])
-            line += f"   hipBLASLt {tr * 1e3:8.1f} us {fl / tr / 1e9:7.1f} TF"
-        print(line, flush=True)
+        for rt in rows:
+            t = min(res[(k, rt)])
+            rtag = f" rows {rt}" if rt is not None else ""
+            line = (f"[cfg {tag}{rtag}] {k:32s} ours {t * 1e3:8.1f} us  {fl / t / 1e9:7.1f} TF "
+                    f"({fl / t / 1e9 / PEAK * 100:4.1f}%)")
+            if ref[k] and rt == rows[0]:
+                tr = min(ref[k])
+                line += f"   hipBLASLt {tr * 1e3:8.1f} us {fl / tr / 1e9:7.1f} TF"
+            print(line, flush=True)
 
 
 if __name__ == "__main__":

@@ -50,11 +50,12 @@ for s in $STEPS; do
       AMD_LOG_LEVEL=1 timeout -k 10 120 python -u tools/fault/run_fault.py > gpurun_out/${TAG}_fault.txt 2>&1
       echo "fault step rc=$?"; grep -v "^:3:" gpurun_out/${TAG}_fault.txt | tail -20; exit 0 ;;
     htrace)  # kernel + HIP API trace of a short bench run: compute-queue gaps vs host API calls
-      timeout -k 10 300 rocprofv3 --kernel-trace --hip-trace -d gpurun_out/${TAG}_htrace -o run -- \
+      timeout -k 10 300 rocprofv3 --kernel-trace --hip-trace --output-format csv -d /tmp/${TAG}_htrace -o run -- \
         python3 bench.py --steps 10 --warmup 5 --no-cpu-baseline --no-traffic --probe-steps 1 > gpurun_out/${TAG}_htrace.json 2>&1 \
         || { tail -20 gpurun_out/${TAG}_htrace.json; exit 1; }
-      d=$(dirname $(find gpurun_out/${TAG}_htrace -name "*kernel_trace.csv" | head -1))
-      python3 tools/host_gaps.py "$d" 3 > gpurun_out/${TAG}_host_gaps.txt 2>&1 || true
+      f=$(find /tmp/${TAG}_htrace -name "*kernel_trace.csv" | head -1)
+      [ -n "$f" ] && python3 tools/host_gaps.py "$(dirname $f)" 3 > gpurun_out/${TAG}_host_gaps.txt 2>&1
+      ls -la $(dirname ${f:-/tmp/x}) >> gpurun_out/${TAG}_host_gaps.txt 2>&1
       head -40 gpurun_out/${TAG}_host_gaps.txt ;;
     fwdcc)  # two concurrent half-batch forwards vs sequential (tools/fwd_concurrency.py)
       timeout -k 10 300 python -u tools/fwd_concurrency.py > gpurun_out/${TAG}_fwd_concurrency.txt 2>&1 \
