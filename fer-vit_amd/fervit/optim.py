@@ -179,6 +179,9 @@ class FusedAdamW(torch.optim.Optimizer):
             e = (dev, len(segs), maxn, sig, counter, tsegs, tiles)
             self._bw_tables[key] = e
         dev, nseg, maxn, _, counter, tsegs, tiles = e
+        if tsegs is None and flat.half_t is not None:  # the transposed copies appeared after the table was built
+            tsegs, tiles = flat.half_t_segments(ps)
+            self._bw_tables[key] = e[:5] + (tsegs, tiles)
         half = flat.bf16()
 
         def launch():

@@ -728,3 +728,28 @@ def test_gemm_row_tile_224_bit_exact(M, N, K, p):
     if p == 0.0:
         ref = x.float() @ w.float().t() + b + res.float()
         assert rel_err(outs[1], ref) < 1e-2
+
+
+def test_gemm_work_queue_every_tile_written():
+    """Work-queue claims of the pipelined plain-kind GEMM (the next tile's claim is an inline-asm atomic
+    whose result is read after the main loop): a NaN-prefilled output must come back finite and equal
+    to torch's product over the whole matrix in every one of several back-to-back launches on one
+    stream (counter bases carried across launches), i.e. no tile skipped or left half-written. The
+    plain kind's arithmetic is idempotent per tile, so a tile processed twice shows up only as the
+    claim count going off, which the next launches would then see as skipped tiles."""
+    from fervit._lib import lib
+
+    o = ops()
+    assert lib().fer_set_persistent_mode(0) == 0
+    g = torch.Generator(device=DEV).manual_seed(17)
+    M, N, K = 50432, 2304, 768
+    x = torch.randn(M, K, device=DEV, generator=g).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV, generator=g) / math.sqrt(K)).to(torch.bfloat16)
+    b = torch.randn(N, device=DEV, generator=g)
+    ref = x.float() @ w.float().t() + b
+    for _ in range(4):
+        y = torch.full((M, N), float("nan"), device=DEV, dtype=torch.bfloat16)
+        o.linear_fwd(x, w, b, out=y)
+        torch.cuda.synchronize()
+        assert torch.isfinite(y.float()).all()
+        assert rel_err(y, ref) < 1e-2

@@ -38,6 +38,7 @@ def main():
     w2t, w1t = w2.t().contiguous(), w1.t().contiguous()  # [F, D], [D, F]
     wo, bo = r(D, D) * 0.03, torch.zeros(D, device=dev)
     q3, wqkvt = r(M, 3 * D), wqkv.t().contiguous()  # dqkv [M, 3D], W_qkv^T [D, 3D]
+    gwq, gwo, gw2 = torch.empty(3 * D, D, device=dev), torch.empty(D, D, device=dev), torch.empty(D, F, device=dev)
     out_f = torch.empty(M, F, device=dev, dtype=torch.bfloat16)
     out_d = torch.empty(M, D, device=dev, dtype=torch.bfloat16)
     cs = torch.zeros(F, device=dev)
@@ -64,6 +65,9 @@ def main():
         "fc1 dgrad +res (B MN, K=3072)": (lambda: ops.linear_dgrad(h, w1, out=out_d, res=x), 2 * M * F * D, None),
         "fc1 dgrad +res (B KC, K=3072)": (lambda: ops.linear_fwd(h, w1t, out=out_d, res=x), 2 * M * F * D, None),
         "fc1 wgrad (MN,MN splitK)": (lambda: ops.linear_wgrad(dF, x, gw), 2 * M * F * D, lambda: dF.t() @ x),
+        "qkv wgrad (MN,MN splitK)": (lambda: ops.linear_wgrad(q3, x, gwq), 2 * M * 3 * D * D, None),
+        "out wgrad (MN,MN splitK)": (lambda: ops.linear_wgrad(x, x, gwo), 2 * M * D * D, None),
+        "fc2 wgrad (MN,MN splitK)": (lambda: ops.linear_wgrad(x, dF, gw2), 2 * M * F * D, None),
         "out-proj fwd +bias+drop+res": (lambda: ops.linear_fwd(x, wo, bo, out=out_d, res=x, dropout=0.1, seed=3),
                                         2 * M * D * D, None),
         "fc2 fwd +bias+drop+res (K=3072)": (lambda: ops.linear_fwd(h, w2, bo, out=out_d, res=x, dropout=0.1, seed=3),

@@ -57,6 +57,12 @@ for s in $STEPS; do
       [ -n "$f" ] && python3 tools/host_gaps.py "$(dirname $f)" 3 > gpurun_out/${TAG}_host_gaps.txt 2>&1
       ls -la $(dirname ${f:-/tmp/x}) >> gpurun_out/${TAG}_host_gaps.txt 2>&1
       head -40 gpurun_out/${TAG}_host_gaps.txt ;;
+    wgcfg)  # weight-gradient GEMMs: the automatic config vs the 8-phase kernel (MT16 / MT32), interleaved runs
+      for c in auto 8 9 auto 8 9; do
+        if [ $c = auto ]; then unset GB_CFG; else export GB_CFG=$c; fi
+        (cd tools && GB_ONLY=wgrad timeout -k 10 200 python -u gemm_bench.py 2>&1 | grep -v amdgpu.ids) \
+          | tee -a gpurun_out/${TAG}_wgrad_cfg.txt || exit 1
+      done; unset GB_CFG ;;
     fwdcc)  # two concurrent half-batch forwards vs sequential (tools/fwd_concurrency.py)
       timeout -k 10 300 python -u tools/fwd_concurrency.py > gpurun_out/${TAG}_fwd_concurrency.txt 2>&1 \
         || { tail -20 gpurun_out/${TAG}_fwd_concurrency.txt; exit 1; }

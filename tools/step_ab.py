@@ -12,6 +12,7 @@ over rounds. Variants:
   both:<p1>/<p2> compute stream on <p1>, weight-gradient stream on <p2>
   wgoff          weight gradients on the compute stream
   adamwbw        FusedAdamW.step_in_backward (per-layer updates from the backward's gradient-ready hook)
+  noadamcache    FusedAdamW uploads its segment table every step (the round-4 behaviour)
   lib:<k>=<v>    a library selector for the variant: attnfwd (fer_attention_set_fwd_kernel), gemmcfg, rowtile
 <pred>: lt<N> (bit < N), ge<N> (bit >= N), m<K>lt<N> (bit % K < N), m<K>ge<N> (bit % K >= N).
 """
@@ -100,6 +101,7 @@ def main():
         lib().fer_gemm_set_config(-1)
         lib().fer_gemm_set_row_tile(256)
         opt.step_in_backward(False)
+        opt.cache_table = True
         runtime.WGRAD.enabled = True
         if "side" not in default_side:  # the shipped side stream (created by the first backward)
             default_side["side"] = runtime.WGRAD.streams.get(dev)
@@ -116,6 +118,8 @@ def main():
             runtime.WGRAD.enabled = False
         elif body == "adamwbw":  # optimizer step inside the backward (FusedAdamW.step_in_backward)
             opt.step_in_backward(True)
+        elif body == "noadamcache":  # FusedAdamW re-uploads its segment table every step (round-4 behaviour)
+            opt.cache_table = False
         elif body.startswith("lib:"):  # a library run-time selector, e.g. lib:attnfwd=2
             k, val = body[4:].split("=")
             fn = {"attnfwd": "fer_attention_set_fwd_kernel", "gemmcfg": "fer_gemm_set_config",
