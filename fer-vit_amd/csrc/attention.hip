@@ -1811,8 +1811,11 @@ extern "C" int64_t fer_attention_ws(int dtype, int B, int N, int H) {
 }
 
 static bool pers_path(int dtype, int N, int dh) { return dtype == FER_BF16 && N <= 224 && dh <= 64; }
-// forward kernel for N <= 224, dh <= 64 (fer_attention_set_fwd_kernel): 1 persistent, 2 occupancy form
-static int g_fwd_kernel = 1;
+// forward kernel for N <= 224, dh <= 64 (fer_attention_set_fwd_kernel): 0 automatic (the occupancy form
+// from 4 query blocks up -- ViT-B/16's N = 197: 36.57 vs 36.87 ms per step on one box, profiles/r05d_* --
+// the persistent kernel below, where its occupancy-sized grids were tuned for the w+ / 48 px token
+// counts), 1 persistent, 2 occupancy form
+static int g_fwd_kernel = 0;
 static int64_t lse_floats(int B, int N, int H) { return ((int64_t)B * H * N + 63) / 64 * 64; }
 // persistent kernels walk a fixed blockIdx stride instead of the work queue (fer_set_persistent_mode)
 static bool fixed_stride() { return fixed_stride_mode(); }
@@ -1873,7 +1876,7 @@ extern "C" int fer_attention_fwd(int dtype, const void* qkv, int64_t ld_qkv, voi
     FER_NB_SWITCH(nb, hipLaunchKernelGGL(attn_fwd_bf16<NB_>, dim3(B * H), dim3(64 * NB_), 0, st, (const bf16*)qkv,
                                          (long)ld_qkv, (bf16*)out, (long)ld_out, lse, N, H, dh, sl2, drop_thresh,
                                          drop_scale, seed));
-  } else if (N <= 224 && dh <= 64 && g_fwd_kernel == 2) {
+  } else if (N <= 224 && dh <= 64 && (g_fwd_kernel == 2 || (g_fwd_kernel == 0 && (N + 31) / 32 >= 4))) {
     const int nb = (N + 31) / 32;
     uint32_t* mask = (drop_thresh && pers_path(dtype, N, dh)) ? (uint32_t*)(lse + lse_floats(B, N, H)) : nullptr;
 #define FER_FOCC2(NBV)                                                                                     \
@@ -2035,6 +2038,6 @@ extern "C" int fer_attention_bwd(int dtype, const void* qkv, int64_t ld_qkv, con
 
 extern "C" int fer_attention_set_fwd_kernel(int k) {
   if (k < 0 || k > 2) return fer::set_error("attention_set_fwd_kernel: 0 (default), 1 (persistent) or 2 (occupancy form)");
-  g_fwd_kernel = k == 0 ? 1 : k;
+  g_fwd_kernel = k;
   return 0;
 }

@@ -152,8 +152,9 @@ int fer_layernorm_bwd(int dtype, const void* dy, int64_t lddy, const void* x, in
  * not re-hash them. bf16: any N, dh <= 128, dh % 8 == 0 (persistent workgroup per CU walking the
  * (batch, head) units for N <= 256 and dh <= 64, 128-row chunks streamed through LDS otherwise). */
 int64_t fer_attention_ws(int dtype, int B, int N, int H);
-/* Forward kernel for bf16, N <= 224, dh <= 64: 0 default, 1 the persistent producer / consumer kernel,
- * 2 the occupancy form (one workgroup per (batch, head), two per CU). Same results bit for bit. */
+/* Forward kernel for bf16, N <= 224, dh <= 64: 0 automatic (the occupancy form for N > 96, else the
+ * persistent kernel), 1 the persistent producer / consumer kernel, 2 the occupancy form (one workgroup
+ * per (batch, head), two per CU). Same results bit for bit. */
 int fer_attention_set_fwd_kernel(int k);
 int64_t fer_attention_saved_floats(int dtype, int B, int N, int H, int dh, uint32_t drop_thresh);
 int fer_attention_fwd(int dtype, const void* qkv, int64_t ld_qkv, void* out, int64_t ld_out, float* saved,

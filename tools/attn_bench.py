@@ -42,7 +42,7 @@ def main():
                 print(f"p={p} fwd kernel {fk}: fwd {tf * 1e3:7.1f} us ({fl_f / tf / 1e9:6.1f} TF, "
                       f"{by_f / tf / 1e6:5.2f} GB/s)   bwd {tb * 1e3:7.1f} us ({2 * fl_f / tb / 1e9:6.1f} TF, "
                       f"{by_b / tb / 1e6:5.2f} GB/s)", flush=True)
-    lib().fer_attention_set_fwd_kernel(0)
+    lib().fer_attention_set_fwd_kernel(0)  # back to automatic
 
 
 if __name__ == "__main__":

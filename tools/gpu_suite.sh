@@ -12,7 +12,7 @@ for s in $STEPS; do
       tail -2 gpurun_out/${TAG}_ktests.txt ;;
     tests)
       timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 150 \
-        --timeout-method thread > gpurun_out/${TAG}_tests.txt 2>&1 || { tail -30 gpurun_out/${TAG}_tests.txt; exit 1; }
+        --timeout-method thread ${TESTS_ARGS:-} > gpurun_out/${TAG}_tests.txt 2>&1 || { tail -30 gpurun_out/${TAG}_tests.txt; exit 1; }
       tail -2 gpurun_out/${TAG}_tests.txt ;;
     bench)
       timeout -k 10 400 python -u bench.py > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err \
@@ -63,6 +63,10 @@ for s in $STEPS; do
         (cd tools && GB_ONLY=wgrad timeout -k 10 200 python -u gemm_bench.py 2>&1 | grep -v amdgpu.ids) \
           | tee -a gpurun_out/${TAG}_wgrad_cfg.txt || exit 1
       done; unset GB_CFG ;;
+    determ)  # run-to-run and 256- vs 224-row bit equality of the residual-kind GEMM
+      timeout -k 10 200 python -u tools/gemm_determinism.py > gpurun_out/${TAG}_determinism.txt 2>&1 \
+        || { tail -20 gpurun_out/${TAG}_determinism.txt; exit 1; }
+      grep -v amdgpu.ids gpurun_out/${TAG}_determinism.txt ;;
     fwdcc)  # two concurrent half-batch forwards vs sequential (tools/fwd_concurrency.py)
       timeout -k 10 300 python -u tools/fwd_concurrency.py > gpurun_out/${TAG}_fwd_concurrency.txt 2>&1 \
         || { tail -20 gpurun_out/${TAG}_fwd_concurrency.txt; exit 1; }
