@@ -63,6 +63,14 @@ for s in $STEPS; do
         (cd tools && GB_ONLY=wgrad timeout -k 10 200 python -u gemm_bench.py 2>&1 | grep -v amdgpu.ids) \
           | tee -a gpurun_out/${TAG}_wgrad_cfg.txt || exit 1
       done; unset GB_CFG ;;
+    gbench)  # GEMM microbenchmark cases whose name contains $GB_ONLY (tools/gemm_bench.py)
+      (cd tools && GB_ONLY="${GB_ONLY:-}" timeout -k 10 300 python -u gemm_bench.py 2>&1 | grep -v amdgpu.ids) \
+        > gpurun_out/${TAG}_gemm_bench.txt || { tail -20 gpurun_out/${TAG}_gemm_bench.txt; exit 1; }
+      cat gpurun_out/${TAG}_gemm_bench.txt ;;
+    ktest)  # the GPU tests whose name matches $KT (pytest -k)
+      timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "$KT" \
+        > gpurun_out/${TAG}_ktest.txt 2>&1 || { tail -30 gpurun_out/${TAG}_ktest.txt; exit 1; }
+      tail -5 gpurun_out/${TAG}_ktest.txt ;;
     determ)  # run-to-run and 256- vs 224-row bit equality of the residual-kind GEMM
       timeout -k 10 200 python -u tools/gemm_determinism.py > gpurun_out/${TAG}_determinism.txt 2>&1 \
         || { tail -20 gpurun_out/${TAG}_determinism.txt; exit 1; }
