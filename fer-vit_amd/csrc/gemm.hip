@@ -931,6 +931,101 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g, 
   tile_epilogue<BM, BN, WM, WN, MT, (BM >= 256 ? 2 : 1), SMEM, EK>(g, e, acc, smem, m0, n0, ks, wm, wn, lane);
 }
 
+// ---- split-K fold (ring launches, fer_gemm_set_splitk_fold): the reduction of the K splits inside
+// the GEMM launch instead of a separate splitk_reduce launch. Every split writes its partial tile to
+// the [split][M][N] fp32 slab with write-through (sc1) stores, drains them and takes a ticket from
+// the tile's counter (agent-scope atomic); the split that draws ticket S-1 reads the S slabs of the
+// tile in split order (sc1 loads, its own included), so the sum is p0 + p1 + ... + p(S-1) whatever
+// the arrival order -- the order splitk_reduce_kernel adds them in, hence bit-identical to it -- and
+// writes c (+)= alpha * sum (the weight-gradient epilogue: fp32 output, optional accumulate). It
+// then resets the counter to 0 for the next launch on its stream (no other split of the tile touches
+// it after the last ticket; the next launch is stream-ordered behind this one). The hand-off is the
+// grouped weight-gradient kernel's (gemm_wgrad_group_kernel, MI355X_MICROARCH.md workgroup
+// dispatch: sc1 stores / counter / acquire + sc1 loads at one workgroup per CU).
+constexpr int FER_TICK_SLOTS = 16, FER_TICK_TILES = 256;
+static __device__ unsigned fer_tick[FER_TICK_SLOTS][FER_TICK_TILES];
+
+template <int BM, int BN, int WM, int WN, int MT, typename AccT, int FN, int FM>
+FER_DEV void splitk_fold(const GemmArgs& g, const EpiArgs& e, AccT (&acc)[FN][FM], char* smem, int tile, int m0,
+                         int n0, int ks, int wm, int wn, int lane) {
+  // whole tiles only (host: M % BM == N % BN == 0, slab and c under 2 GiB): one per-lane offset, the
+  // (split, block) part in the scalar offset
+  constexpr int TM = BM / WM, TN = BN / WN;
+  constexpr int NQ = MT == 32 ? 4 : 1;
+  const int lr = MT == 32 ? (lane & 31) : (lane & 15);
+  const int lc = MT == 32 ? 4 * (lane >> 5) : 4 * (lane >> 4);
+  const int S = g.splits;
+  const __amdgpu_buffer_rsrc_t rs = make_rsrc(g.ws);
+  const uint32_t lo = (uint32_t)(((m0 + wm * TM + lr) * g.N + n0 + wn * TN + lc) * 4);
+  auto so = [&](int sp, int i, int j, int q) -> int {  // element (j*MT, i*MT + 8q) of split sp
+    return __builtin_amdgcn_readfirstlane((int)((((long)sp * g.M + j * MT) * g.N + i * MT + 8 * q) * 4));
+  };
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int j = 0; j < FM; ++j)
+#pragma unroll
+      for (int q = 0; q < NQ; ++q)
+        __builtin_amdgcn_raw_buffer_store_b128(
+            __builtin_bit_cast(u32x4, f32x4{acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]}),
+            rs, lo, so(ks, i, j, q), 16 /* sc1: write-through */);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's partial drained
+  __syncthreads();  // every wave's partial drained; every wave is past its last LDS read
+  lds_vuint* flag = FER_LDS_UINT(smem);
+  if (threadIdx.x == 0) {
+    const unsigned tk = __hip_atomic_fetch_add(g.tick + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tk == (unsigned)(S - 1)) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      __hip_atomic_store(g.tick + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    *flag = tk;
+  }
+  __syncthreads();
+  if (*flag != (unsigned)(S - 1)) return;  // not the last split of this tile
+  // one accumulator column block (i) at a time -- its S slabs in split order, then c (+)= alpha * sum in
+  // epi4's order for an fp32 output with no other epilogue operand -- so only FM x NQ loaded pieces are
+  // live beside the accumulators (summing or writing the whole tile at once spilled)
+  const __amdgpu_buffer_rsrc_t rc = make_rsrc(e.c);
+  const uint32_t co = (uint32_t)(((long)(m0 + wm * TM + lr) * e.ldc + n0 + wn * TN + lc) * 4);
+#pragma unroll
+  for (int i = 0; i < FN; ++i) {
+#pragma unroll 1
+    for (int sp = 0; sp < S; ++sp) {
+      f32x4 v[FM][NQ];
+#pragma unroll
+      for (int j = 0; j < FM; ++j)
+#pragma unroll
+        for (int q = 0; q < NQ; ++q)
+          v[j][q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, lo, so(sp, i, j, q), 16));
+#pragma unroll
+      for (int j = 0; j < FM; ++j)
+#pragma unroll
+        for (int q = 0; q < NQ; ++q)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[i][j][4 * q + r] = sp ? acc[i][j][4 * q + r] + v[j][q][r] : v[j][q][r];
+    }
+    f32x4 cv[FM][NQ];
+#pragma unroll
+    for (int j = 0; j < FM; ++j)
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const int cs = __builtin_amdgcn_readfirstlane((int)(((long)j * MT * e.ldc + i * MT + 8 * q) * 4));
+        cv[j][q] = e.accumulate ? __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rc, co, cs, 0))
+                                : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+    for (int j = 0; j < FM; ++j)
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const int cs = __builtin_amdgcn_readfirstlane((int)(((long)j * MT * e.ldc + i * MT + 8 * q) * 4));
+        f32x4 v = f32x4{acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]};
+        v *= e.alpha;
+        if (e.accumulate) v += cv[j][q];
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rc, co, cs, 0);
+      }
+  }
+}
+
 // Ring variant: BK=32 stages in an NST-slot LDS ring, LDS-DMA issued NST-1 K-steps ahead and
 // spread over the substeps (so no wave blocks on a burst of DMA issue and each stage has
 // ~NST-2 K-steps to land). Per K-step t, in its last substep: counted vmcnt for stage t+1,
@@ -1054,6 +1149,13 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_ring_kernel(GemmArgs g, 
       for (int i = 0; i < FN; ++i) bfr[i] = bn[i];
 #pragma unroll
       for (int j = 0; j < FM; ++j) af[j] = an[j];
+    }
+  }
+  // (not in the 256^2 MT32 form, cfg 4: its 4 x 4-register row pieces per column block spill)
+  if constexpr (MT == 16 || BM < 256) {
+    if (g.tick) {
+      splitk_fold<BM, BN, WM, WN, MT>(g, e, acc, smem, tm * g.tiles_n + tn, m0, n0, ks, wm, wn, lane);
+      return;
     }
   }
   tile_epilogue<BM, BN, WM, WN, MT, EPC, NST * STAGE>(g, e, acc, smem, m0, n0, ks, wm, wn, lane);
@@ -2143,6 +2245,37 @@ static int dispatch_tile(int cfg, GemmArgs g, const EpiArgs& e, hipStream_t st) 
   }
 }
 
+// Host: the tile-ticket counters of the split-K fold for launches on `st` (null: none left -- the
+// launch then reduces with splitk_reduce_kernel). One slot of fer_tick per (device, stream), as the
+// work queues: concurrent ring launches on different streams never share counters.
+static int g_fold = 1;  // fer_gemm_set_splitk_fold
+static unsigned* tick_slot(hipStream_t st) {
+  static std::mutex mu;
+  static std::map<std::pair<int, hipStream_t>, unsigned*> slots;
+  static std::map<int, std::pair<unsigned*, int>> pools;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lk(mu);
+  const auto key = std::make_pair(dev, st);
+  auto it = slots.find(key);
+  if (it != slots.end()) return it->second;
+  auto pit = pools.find(dev);
+  if (pit == pools.end()) {
+    unsigned* pool = nullptr;
+    if (hipGetSymbolAddress((void**)&pool, HIP_SYMBOL(fer_tick)) != hipSuccess) pool = nullptr;
+    pit = pools.emplace(dev, std::make_pair(pool, 0)).first;
+  }
+  if (!pit->second.first || pit->second.second >= FER_TICK_SLOTS) return nullptr;
+  unsigned* s = pit->second.first + FER_TICK_TILES * pit->second.second++;
+  slots.emplace(key, s);
+  return s;
+}
+// epilogues the fold implements: fp32 output (+ accumulate, alpha), nothing else
+static bool fold_epilogue(const EpiArgs& e) {
+  return e.c_f32 && !e.bias && !(e.act & 15) && !e.pre && !e.res && !e.drop_thresh && !e.aux && !e.post_scale &&
+         !e.colsum;
+}
+
 int gemm_launch(const GemmDesc& d, const EpiArgs& e_in, hipStream_t st) {
   EpiArgs e = e_in;
   GemmArgs g{};
@@ -2225,6 +2358,13 @@ int gemm_launch(const GemmDesc& d, const EpiArgs& e_in, hipStream_t st) {
   if (splits > 1) g.splits = (d.K + g.k_chunk - 1) / g.k_chunk;
   g.partial = g.splits > 1;
   g.ws = d.ws;
+  if (g.partial && g_fold && cfg >= 5 && cfg <= 7 && fold_epilogue(e)) {
+    const int bt = cfg == 5 ? 256 : 128;
+    const long tiles = (long)((d.M + bt - 1) / bt) * ((d.N + bt - 1) / bt);
+    if (tiles <= FER_TICK_TILES && d.M % bt == 0 && d.N % bt == 0 && (long)g.splits * d.M * d.N * 4 < 0x7FFFFFF0L &&
+        ((long)(d.M - 1) * e.ldc + d.N) * 4 < 0x7FFFFFF0L)
+      g.tick = tick_slot(st);
+  }
   g.cs_part = e.colsum ? reduction_ws(d.ws, (size_t)((d.M + (cfg_is_256(cfg) ? 255 : 127)) / (cfg_is_256(cfg) ? 256 : 128)) * d.N * 4,
                                       d.N, st)
                        : nullptr;
@@ -2239,7 +2379,7 @@ int gemm_launch(const GemmDesc& d, const EpiArgs& e_in, hipStream_t st) {
                 nullptr, st);
     rc = hip_check("gemm_colsum_reduce");
   }
-  if (rc || !g.partial) return rc;
+  if (rc || !g.partial || g.tick) return rc;
   const long work = (long)d.M * (d.N / 4);
   const int blocks = (int)std::min<long>((work + 255) / 256, 4096);
   hipLaunchKernelGGL(splitk_reduce_kernel<bf16>, dim3(blocks), dim3(256), 0, st, d.ws, g.splits, (long)d.M,
@@ -2329,6 +2469,11 @@ int fer::set_step_ptr_gemm(const uint64_t* p) { return set_step_ptr_here(p) == h
 extern "C" int64_t fer_gemm_colsum_ws(int M, int N) {
   // tile partials (128-row tiles at most) or the stand-alone colsum pass's partials
   return (int64_t)std::max(fer::ceil_div(std::max(M, 1), 128), 256) * N * 4;
+}
+
+extern "C" int fer_gemm_set_splitk_fold(int on) {
+  fer::g_fold = on ? 1 : 0;
+  return 0;
 }
 
 extern "C" int fer_gemm_set_row_tile(int rows) {

@@ -753,3 +753,46 @@ def test_gemm_work_queue_every_tile_written():
         torch.cuda.synchronize()
         assert torch.isfinite(y.float()).all()
         assert rel_err(y, ref) < 1e-2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K,acc", [(50432, 3072, 768, False), (50432, 768, 768, True), (20000, 1000, 264, True),
+                                       (16384, 2304, 768, False)])
+def test_wgrad_splitk_fold_bit_exact(M, N, K, acc):
+    """Split-K weight gradients (MN x MN ring kernel) with the in-launch fold (fer_gemm_set_splitk_fold(1),
+    tile tickets, last split sums the slabs in split order; whole tiles only -- the 1000 x 264 case takes
+    the separate reduction either way) against the separate reduction launch:
+    bit-identical, bit-identical run to run, every element written (NaN prefill when not accumulating),
+    and within bf16-input tolerance of the fp32 product. Also two streams folding at once (separate
+    ticket slots)."""
+    from fervit._lib import lib
+
+    o = ops()
+    g = torch.Generator(device=DEV).manual_seed(M + N + K)
+    dy = torch.randn(M, N, device=DEV, generator=g).to(torch.bfloat16)
+    x = torch.randn(M, K, device=DEV, generator=g).to(torch.bfloat16)
+    c0 = torch.randn(N, K, device=DEV, generator=g) if acc else torch.full((N, K), float("nan"), device=DEV)
+    outs = []
+    try:
+        for fold in (0, 1, 1):
+            lib().fer_gemm_set_splitk_fold(fold)
+            c = c0.clone()
+            o.linear_wgrad(dy, x, c, accumulate=acc)
+            torch.cuda.synchronize()
+            outs.append(c)
+        # two streams at once, both folding
+        s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+        ca, cb = c0.clone(), c0.clone()
+        torch.cuda.synchronize()
+        with torch.cuda.stream(s1):
+            o.linear_wgrad(dy, x, ca, accumulate=acc)
+        with torch.cuda.stream(s2):
+            o.linear_wgrad(dy, x, cb, accumulate=acc)
+        torch.cuda.synchronize()
+    finally:
+        lib().fer_gemm_set_splitk_fold(1)
+    assert torch.isfinite(outs[1]).all()
+    for c in outs[1:] + [ca, cb]:
+        assert torch.equal(c.view(torch.int32), outs[0].view(torch.int32))
+    ref = dy.float().t() @ x.float() + (c0 if acc else 0)
+    assert rel_err(outs[1], ref) < 1e-3

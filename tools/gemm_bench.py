@@ -82,30 +82,37 @@ def main():
     only = os.environ.get("GB_ONLY")
     if only:
         cases = {k: v for k, v in cases.items() if only in k}
-    # GB_ROWS=ab: every case at both row tiles of fer_gemm_set_row_tile (256, 224), interleaved
-    rows = [256, 224] if os.environ.get("GB_ROWS") == "ab" else [None]
+    # GB_ROWS=ab: every case at both row tiles of fer_gemm_set_row_tile (256, 224), interleaved;
+    # GB_FOLD=ab: split-K reduction in the launch (fer_gemm_set_splitk_fold 1) and as its own launch (0)
     from fervit._lib import lib
 
-    res = {(k, rt): [] for k in cases for rt in rows}
+    if os.environ.get("GB_ROWS") == "ab":
+        rows = [("rows 256", lambda: lib().fer_gemm_set_row_tile(256)), ("rows 224", lambda: lib().fer_gemm_set_row_tile(224))]
+    elif os.environ.get("GB_FOLD") == "ab":
+        rows = [("fold 1", lambda: lib().fer_gemm_set_splitk_fold(1)), ("fold 0", lambda: lib().fer_gemm_set_splitk_fold(0))]
+    else:
+        rows = [(None, None)]
+
+    res = {(k, rt): [] for k in cases for rt, _ in rows}
     ref = {k: [] for k in cases}
     for _ in range(3):
         for k, (fn, fl, tf) in cases.items():
-            for rt in rows:
-                if rt is not None:
-                    lib().fer_gemm_set_row_tile(rt)
+            for rt, setv in rows:
+                if setv is not None:
+                    setv()
                 res[(k, rt)].append(timeit(fn))
             if tf is not None:
                 ref[k].append(timeit(tf))
-    if rows[0] is not None:
-        lib().fer_gemm_set_row_tile(256)
+    lib().fer_gemm_set_row_tile(256)
+    lib().fer_gemm_set_splitk_fold(1)
     tag = cfg if cfg is not None else "auto"
     for k, (fn, fl, tf) in cases.items():
-        for rt in rows:
+        for rt, _ in rows:
             t = min(res[(k, rt)])
-            rtag = f" rows {rt}" if rt is not None else ""
+            rtag = f" {rt}" if rt is not None else ""
             line = (f"[cfg {tag}{rtag}] {k:32s} ours {t * 1e3:8.1f} us  {fl / t / 1e9:7.1f} TF "
                     f"({fl / t / 1e9 / PEAK * 100:4.1f}%)")
-            if ref[k] and rt == rows[0]:
+            if ref[k] and rt == rows[0][0]:
                 tr = min(ref[k])
                 line += f"   hipBLASLt {tr * 1e3:8.1f} us {fl / tr / 1e9:7.1f} TF"
             print(line, flush=True)
