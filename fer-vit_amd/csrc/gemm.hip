@@ -960,22 +960,30 @@ FER_DEV void splitk_fold(const GemmArgs& g, const EpiArgs& e, AccT (&acc)[FN][FM
   auto so = [&](int sp, int i, int j, int q) -> int {  // element (j*MT, i*MT + 8q) of split sp
     return __builtin_amdgcn_readfirstlane((int)((((long)sp * g.M + j * MT) * g.N + i * MT + 8 * q) * 4));
   };
+  const bool plain = g.partial == 3;  // (diagnostic: plain stores / loads + agent release and acquire)
 #pragma unroll
   for (int i = 0; i < FN; ++i)
 #pragma unroll
     for (int j = 0; j < FM; ++j)
 #pragma unroll
-      for (int q = 0; q < NQ; ++q)
-        __builtin_amdgcn_raw_buffer_store_b128(
-            __builtin_bit_cast(u32x4, f32x4{acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]}),
-            rs, lo, so(ks, i, j, q), 16 /* sc1: write-through */);
+      for (int q = 0; q < NQ; ++q) {
+        const u32x4 d = __builtin_bit_cast(u32x4, f32x4{acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2],
+                                                        acc[i][j][4 * q + 3]});
+        if (plain) __builtin_amdgcn_raw_buffer_store_b128(d, rs, lo, so(ks, i, j, q), 0);
+        else __builtin_amdgcn_raw_buffer_store_b128(d, rs, lo, so(ks, i, j, q), 16 /* sc1: write-through */);
+      }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's partial drained
   __syncthreads();  // every wave's partial drained; every wave is past its last LDS read
   lds_vuint* flag = FER_LDS_UINT(smem);
   if (threadIdx.x == 0) {
+    if (plain) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     const unsigned tk = __hip_atomic_fetch_add(g.tick + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (tk == (unsigned)(S - 1)) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __hip_atomic_store(g.tick + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     *flag = tk;
@@ -996,13 +1004,23 @@ FER_DEV void splitk_fold(const GemmArgs& g, const EpiArgs& e, AccT (&acc)[FN][FM
       for (int j = 0; j < FM; ++j)
 #pragma unroll
         for (int q = 0; q < NQ; ++q)
-          v[j][q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, lo, so(sp, i, j, q), 16));
+          v[j][q] = plain ? __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, lo, so(sp, i, j, q), 0))
+                          : __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, lo, so(sp, i, j, q), 16));
 #pragma unroll
       for (int j = 0; j < FM; ++j)
 #pragma unroll
         for (int q = 0; q < NQ; ++q)
 #pragma unroll
           for (int r = 0; r < 4; ++r) acc[i][j][4 * q + r] = sp ? acc[i][j][4 * q + r] + v[j][q][r] : v[j][q][r];
+    }
+    if (g.partial == 4) {  // (diagnostic: the sum also into split slot S of the slab)
+#pragma unroll
+      for (int j = 0; j < FM; ++j)
+#pragma unroll
+        for (int q = 0; q < NQ; ++q)
+          __builtin_amdgcn_raw_buffer_store_b128(
+              __builtin_bit_cast(u32x4, f32x4{acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]}),
+              rs, lo, so(S, i, j, q), 0);
     }
     f32x4 cv[FM][NQ];
 #pragma unroll
@@ -1019,7 +1037,7 @@ FER_DEV void splitk_fold(const GemmArgs& g, const EpiArgs& e, AccT (&acc)[FN][FM
       for (int q = 0; q < NQ; ++q) {
         const int cs = __builtin_amdgcn_readfirstlane((int)(((long)j * MT * e.ldc + i * MT + 8 * q) * 4));
         f32x4 v = f32x4{acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]};
-        v *= e.alpha;
+        if (g.partial != 2) v *= e.alpha;  // (2: alpha == 1, diagnostic mode of fer_gemm_set_splitk_fold)
         if (e.accumulate) v += cv[j][q];
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rc, co, cs, 0);
       }
@@ -2364,6 +2382,9 @@ int gemm_launch(const GemmDesc& d, const EpiArgs& e_in, hipStream_t st) {
     if (tiles <= FER_TICK_TILES && d.M % bt == 0 && d.N % bt == 0 && (long)g.splits * d.M * d.N * 4 < 0x7FFFFFF0L &&
         ((long)(d.M - 1) * e.ldc + d.N) * 4 < 0x7FFFFFF0L)
       g.tick = tick_slot(st);
+    if (g.tick && g_fold == 2 && e.alpha == 1.f) g.partial = 2;
+    if (g.tick && g_fold == 3) g.partial = 3;
+    if (g.tick && g_fold == 4 && (long)(g.splits + 1) * d.M * d.N * 4 <= d.ws_bytes) g.partial = 4;
   }
   g.cs_part = e.colsum ? reduction_ws(d.ws, (size_t)((d.M + (cfg_is_256(cfg) ? 255 : 127)) / (cfg_is_256(cfg) ? 256 : 128)) * d.N * 4,
                                       d.N, st)
@@ -2472,7 +2493,7 @@ extern "C" int64_t fer_gemm_colsum_ws(int M, int N) {
 }
 
 extern "C" int fer_gemm_set_splitk_fold(int on) {
-  fer::g_fold = on ? 1 : 0;
+  fer::g_fold = on;
   return 0;
 }
 

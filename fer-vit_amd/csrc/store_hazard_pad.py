@@ -1,0 +1,126 @@
+"""Build step: pad gfx950 device assembly so that no VALU instruction overwrites a VGPR / AGPR that a
+preceding vector-memory store reads (its data or its address) within W issue slots.
+
+Why: on MI355X the hardware read of a store's operands can trail its issue by more than the wait
+states the compiler accounts for (LLVM pads a VALU write of a >8-byte store's data by 2 wait states on
+gfx940+, and the address not at all). Measured here (profiles/r05_store_war_*):
+  * a dwordx4 buffer store, two SALU instructions, then a v_pk_mul_f32 writing the store's first data
+    pair: the store wrote the new value of one dword in lanes 12-15 of every 16 (the in-launch split-K
+    fold, every launch);
+  * the 128^2 GEMM's staged epilogue: a global_store_dwordx4 whose address pair is advanced by a
+    v_lshl_add_u64 four slots later: one 8-row pass of a tile left unwritten about once in 40 launches.
+The pass walks each store's following instructions in program order; when a VALU (v_*) or an LDS read writes one of
+the store's registers less than W slots after it, an s_nop of the missing slots goes in front of that
+instruction. A window that reaches a label or branch first is padded there (the successor is not
+followed). Every other instruction is left as it is.
+
+    python store_hazard_pad.py in.s out.s [W]
+"""
+import re
+import sys
+
+W_DEFAULT = 16
+
+STORE = re.compile(r"^\s*(global|buffer|flat|scratch)_store_\w+")
+BRANCH = re.compile(r"^\s*s_(branch|cbranch_\w+|setpc_b64|swappc_b64|endpgm\w*)\b")
+LABEL = re.compile(r"^[.\w$]+:")
+REG = re.compile(r"\b([va])(\d+)\b|\b([va])\[(\d+):(\d+)\]")
+
+
+def regs(text):
+    out = set()
+    for m in REG.finditer(text):
+        if m.group(1):
+            out.add((m.group(1), int(m.group(2))))
+        else:
+            out.update((m.group(3), r) for r in range(int(m.group(4)), int(m.group(5)) + 1))
+    return out
+
+
+def store_regs(line):
+    """Registers a store reads: every v/a register among its operands (data and address)."""
+    body = line.split(None, 1)[1] if len(line.split(None, 1)) > 1 else ""
+    body = body.split("//")[0].split(";")[0]
+    return regs(body)
+
+
+def valu_dst(line):
+    """Registers written soon after issue: VALU destinations and LDS-load destinations (an LDS read
+    returns within tens of cycles; vector-memory loads return far later and are not tracked)."""
+    t = line.strip()
+    if not (t.startswith("v_") or t.startswith("ds_read") or t.startswith("ds_load")):
+        return set()
+    parts = t.split(None, 1)
+    if len(parts) < 2:
+        return set()
+    first = parts[1].split(",")[0].strip()
+    return regs(first)
+
+
+def slots(line):
+    t = line.strip()
+    m = re.match(r"s_nop\s+(\d+)", t)
+    if m:
+        return int(m.group(1)) + 1
+    return 1
+
+
+def is_instr(line):
+    t = line.strip()
+    return bool(t) and not t.startswith((".", ";", "//")) and not LABEL.match(t)
+
+
+def nops(n, indent="\t"):
+    out = []
+    while n > 0:
+        k = min(n, 8)
+        out.append(f"{indent}s_nop {k - 1}\t; store operand hazard pad\n")
+        n -= k
+    return out
+
+
+def pad(lines, W):
+    insert_before = {}  # line index -> slots to pad in front of it
+    for i, l in enumerate(lines):
+        if not STORE.match(l):
+            continue
+        live = store_regs(l)
+        if not live:
+            continue
+        used = 0
+        for j in range(i + 1, len(lines)):
+            t = lines[j]
+            if LABEL.match(t.strip()) or BRANCH.match(t):
+                if used < W:
+                    insert_before[j] = max(insert_before.get(j, 0), W - used)
+                break
+            if not is_instr(t):
+                continue
+            if valu_dst(t) & live:
+                if used < W:
+                    insert_before[j] = max(insert_before.get(j, 0), W - used)
+                break
+            used += slots(t)
+            if used >= W:
+                break
+    out = []
+    for i, l in enumerate(lines):
+        if i in insert_before:
+            out.extend(nops(insert_before[i]))
+        out.append(l)
+    return out, len(insert_before)
+
+
+def main():
+    src, dst = sys.argv[1], sys.argv[2]
+    W = int(sys.argv[3]) if len(sys.argv) > 3 else W_DEFAULT
+    with open(src) as f:
+        lines = f.readlines()
+    out, n = pad(lines, W)
+    with open(dst, "w") as f:
+        f.writelines(out)
+    print(f"store_hazard_pad: {n} pads ({W} slots) in {src}", file=sys.stderr)
+
+
+if __name__ == "__main__":
+    main()

@@ -772,14 +772,17 @@ def test_wgrad_splitk_fold_bit_exact(M, N, K, acc):
     dy = torch.randn(M, N, device=DEV, generator=g).to(torch.bfloat16)
     x = torch.randn(M, K, device=DEV, generator=g).to(torch.bfloat16)
     c0 = torch.randn(N, K, device=DEV, generator=g) if acc else torch.full((N, K), float("nan"), device=DEV)
-    outs = []
+    outs, slabs = [], []
+    from fervit import ops as fops
     try:
-        for fold in (0, 1, 1):
+        for fold in (0, 1, 1, 2, 3):
             lib().fer_gemm_set_splitk_fold(fold)
             c = c0.clone()
             o.linear_wgrad(dy, x, c, accumulate=acc)
             torch.cuda.synchronize()
             outs.append(c)
+            ws = [b for k, b in fops.WS.buf.items() if k[1] == 1 and k[2] == torch.cuda.current_stream().cuda_stream]
+            slabs.append(ws[0][: 8 * N * K].clone() if ws else None)
         # two streams at once, both folding
         s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
         ca, cb = c0.clone(), c0.clone()
@@ -792,7 +795,24 @@ def test_wgrad_splitk_fold_bit_exact(M, N, K, acc):
     finally:
         lib().fer_gemm_set_splitk_fold(1)
     assert torch.isfinite(outs[1]).all()
-    for c in outs[1:] + [ca, cb]:
-        assert torch.equal(c.view(torch.int32), outs[0].view(torch.int32))
+    bad = []
+    for name, c in zip(("fold", "fold again", "fold without alpha", "fold plain+fences", "stream 1", "stream 2"),
+                       outs[1:] + [ca, cb]):
+        d = c.view(torch.int32) != outs[0].view(torch.int32)
+        if d.any():
+            idx = d.nonzero()
+            t = torch.unique((idx[:, 0] // 256) * 1000 + idx[:, 1] // 256)
+            ex = (c[d] - outs[0][d]).abs().max().item()
+            rr = torch.bincount(idx[:, 0] % 256, minlength=256).nonzero().flatten()
+            cc = torch.bincount(idx[:, 1] % 256, minlength=256).nonzero().flatten()
+            ratio = (c[d] / outs[0][d])[:6].tolist()
+            bad.append(f"{name}: {int(d.sum())} elements, tiles (row*1000+col) {t[:12].tolist()}, max |diff| {ex:.3g}, "
+                       f"rows%256 {rr[:24].tolist()} ({len(rr)}), cols%256 {cc[:24].tolist()} ({len(cc)}), "
+                       f"ratio fold/ref {[round(v, 3) for v in ratio]}")
+    if bad and slabs[0] is not None:  # were the split partials themselves stored differently?
+        for f, sl in zip((1, 1, 2, 3), slabs[1:]):
+            d = sl.view(torch.int32) != slabs[0].view(torch.int32)
+            bad.append(f"slab fold {f}: {int(d.sum())} words differ from the reduction run's")
+    assert not bad, "; ".join(bad)
     ref = dy.float().t() @ x.float() + (c0 if acc else 0)
     assert rel_err(outs[1], ref) < 1e-3

@@ -14,7 +14,38 @@ from fervit import ops  # noqa: E402
 from fervit._lib import lib  # noqa: E402
 
 
+def stress(reps):
+    """GD_STRESS=<reps>: the residual launch of the row-tile test's failing case (M 20000, N 768, K 3072,
+    automatic configuration: 128^2 tiles) repeated, every repeat compared bit for bit with the first."""
+    dev = "cuda"
+    M, N, K = 20000, 768, 3072
+    g = torch.Generator(device=dev).manual_seed(M + N + K)
+    x = torch.randn(M, K, device=dev, generator=g).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=dev, generator=g) / math.sqrt(K)).to(torch.bfloat16)
+    b = torch.randn(N, device=dev, generator=g)
+    res = torch.randn(M, N, device=dev, generator=g).to(torch.bfloat16)
+    first, nbad = None, 0
+    for r in range(reps):
+        y = torch.full((M, N), float("nan"), device=dev, dtype=torch.bfloat16)
+        ops.linear_fwd(x, w, b, out=y, res=res, dropout=0.0, seed=1234, drop_ld=N)
+        torch.cuda.synchronize()
+        yi = y.view(torch.int16).clone()
+        if first is None:
+            first = yi
+            continue
+        d = yi != first
+        if d.any():
+            nbad += 1
+            idx = d.nonzero()
+            print(f"repeat {r}: {int(d.sum())} elements differ, rows {idx[:6, 0].tolist()} cols {idx[:6, 1].tolist()}, "
+                  f"row%128 {torch.unique(idx[:, 0] % 128)[:16].tolist()}", flush=True)
+    print(f"stress: {nbad} of {reps - 1} repeats differ from the first", flush=True)
+
+
 def main():
+    if os.environ.get("GD_STRESS"):
+        stress(int(os.environ["GD_STRESS"]))
+        return
     dev = "cuda"
     for (M, N, K) in [(20000, 768, 3072), (50432, 768, 768), (50432, 768, 3072), (20000, 768, 1536)]:
         g = torch.Generator(device=dev).manual_seed(M + N + K)
