@@ -775,7 +775,7 @@ def test_wgrad_splitk_fold_bit_exact(M, N, K, acc):
     outs, slabs = [], []
     from fervit import ops as fops
     try:
-        for fold in (0, 1, 1, 2, 3):
+        for fold in (0, 1, 1):
             lib().fer_gemm_set_splitk_fold(fold)
             c = c0.clone()
             o.linear_wgrad(dy, x, c, accumulate=acc)
@@ -796,8 +796,7 @@ def test_wgrad_splitk_fold_bit_exact(M, N, K, acc):
         lib().fer_gemm_set_splitk_fold(1)
     assert torch.isfinite(outs[1]).all()
     bad = []
-    for name, c in zip(("fold", "fold again", "fold without alpha", "fold plain+fences", "stream 1", "stream 2"),
-                       outs[1:] + [ca, cb]):
+    for name, c in zip(("fold", "fold again", "stream 1", "stream 2"), outs[1:] + [ca, cb]):
         d = c.view(torch.int32) != outs[0].view(torch.int32)
         if d.any():
             idx = d.nonzero()
@@ -810,7 +809,7 @@ def test_wgrad_splitk_fold_bit_exact(M, N, K, acc):
                        f"rows%256 {rr[:24].tolist()} ({len(rr)}), cols%256 {cc[:24].tolist()} ({len(cc)}), "
                        f"ratio fold/ref {[round(v, 3) for v in ratio]}")
     if bad and slabs[0] is not None:  # were the split partials themselves stored differently?
-        for f, sl in zip((1, 1, 2, 3), slabs[1:]):
+        for f, sl in zip((1, 1), slabs[1:]):
             d = sl.view(torch.int32) != slabs[0].view(torch.int32)
             bad.append(f"slab fold {f}: {int(d.sum())} words differ from the reduction run's")
     assert not bad, "; ".join(bad)

@@ -21,7 +21,7 @@ def main():
     dy = torch.randn(M, N, device=dev, generator=g).to(torch.bfloat16)
     x = torch.randn(M, K, device=dev, generator=g).to(torch.bfloat16)
     outs = []
-    for fold in (0, int(os.environ.get('FOLD_MODE', '4'))):
+    for fold in (0, 1):
         lib().fer_gemm_set_splitk_fold(fold)
         c = torch.full((N, K), float("nan"), device=dev)
         ops.linear_wgrad(dy, x, c)
@@ -35,10 +35,6 @@ def main():
     for s in range(1, S):
         ssum += slab[s]
     print("reduction path == sum of slabs in split order:", torch.equal(ssum, outs[0]))
-    dbg = ws[S * N * K: (S + 1) * N * K].view(N, K)
-    print("fold's sum (slot S) == reference sum:", torch.equal(dbg, ssum),
-          " differing:", int((dbg != ssum).sum()), " fold's c == its own sum:", torch.equal(dbg, outs[1]),
-          " differing:", int((dbg != outs[1]).sum()))
     d = (outs[1] != outs[0]).nonzero()
     print("differing elements:", d.shape[0])
     for r, c in d[:6].tolist():

@@ -37,8 +37,15 @@ def stress(reps):
         if d.any():
             nbad += 1
             idx = d.nonzero()
-            print(f"repeat {r}: {int(d.sum())} elements differ, rows {idx[:6, 0].tolist()} cols {idx[:6, 1].tolist()}, "
+            bad = y[d].float()
+            rows = torch.unique(idx[:, 0])
+            cols = torch.unique(idx[:, 1])
+            print(f"repeat {r}: {int(d.sum())} elements differ, NaN (unwritten) {int(torch.isnan(bad).sum())}, "
+                  f"rows {rows[:16].tolist()} ({len(rows)}), cols {cols.min().item()}..{cols.max().item()} ({len(cols)}), "
+                  f"tiles(128) {torch.unique((idx[:, 0] // 128) * 100 + idx[:, 1] // 128)[:8].tolist()}, "
                   f"row%128 {torch.unique(idx[:, 0] % 128)[:16].tolist()}", flush=True)
+            good = first.view(torch.bfloat16)[d].float()
+            print(f"   got {bad[:6].tolist()} expected {good[:6].tolist()}", flush=True)
     print(f"stress: {nbad} of {reps - 1} repeats differ from the first", flush=True)
 
 
