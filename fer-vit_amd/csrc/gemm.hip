@@ -1000,20 +1000,29 @@ FER_DEV void splitk_fold(const GemmArgs& g, const EpiArgs& e, AccT (&acc)[FN][FM
   const uint32_t co = (uint32_t)(((long)(m0 + wm * TM + lr) * e.ldc + n0 + wn * TN + lc) * 4);
 #pragma unroll
   for (int i = 0; i < FN; ++i) {
+    // two splits per round (2 x FM x NQ loads in flight): the reading split runs alone on its CU
+    // and its reads are latency-bound; the sum stays p0 + p1 + ... in split order
 #pragma unroll 1
-    for (int sp = 0; sp < S; ++sp) {
-      f32x4 v[FM][NQ];
+    for (int sp = 0; sp < S; sp += 2) {
+      const bool two = sp + 1 < S;
+      f32x4 v[FM][NQ], w[FM][NQ];
 #pragma unroll
       for (int j = 0; j < FM; ++j)
 #pragma unroll
-        for (int q = 0; q < NQ; ++q)
+        for (int q = 0; q < NQ; ++q) {
           v[j][q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, lo, so(sp, i, j, q), 16));
+          w[j][q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, two ? lo : FER_OOB,
+                                                                                    so(sp + 1, i, j, q), 16));
+        }
 #pragma unroll
       for (int j = 0; j < FM; ++j)
 #pragma unroll
         for (int q = 0; q < NQ; ++q)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) acc[i][j][4 * q + r] = sp ? acc[i][j][4 * q + r] + v[j][q][r] : v[j][q][r];
+          for (int r = 0; r < 4; ++r) {
+            float a = sp ? acc[i][j][4 * q + r] + v[j][q][r] : v[j][q][r];
+            acc[i][j][4 * q + r] = two ? a + w[j][q][r] : a;
+          }
     }
     f32x4 cv[FM][NQ];
 #pragma unroll
@@ -2259,7 +2268,10 @@ static int dispatch_tile(int cfg, GemmArgs g, const EpiArgs& e, hipStream_t st) 
 // Host: the tile-ticket counters of the split-K fold for launches on `st` (null: none left -- the
 // launch then reduces with splitk_reduce_kernel). One slot of fer_tick per (device, stream), as the
 // work queues: concurrent ring launches on different streams never share counters.
-static int g_fold = 1;  // fer_gemm_set_splitk_fold
+// (off by default: the reading split runs alone on its CU, and reading S slabs there costs more than the
+// separate reduction launch -- fc1 / qkv / out_proj / fc2 weight gradients alone 301 / 277 / 250 / 316 us
+// folded vs 254 / 203 / 89 / 262 us with the launch, the step 36.83 vs 36.62 ms: profiles/r05r_*)
+static int g_fold = 0;  // fer_gemm_set_splitk_fold
 static unsigned* tick_slot(hipStream_t st) {
   static std::mutex mu;
   static std::map<std::pair<int, hipStream_t>, unsigned*> slots;

@@ -81,9 +81,9 @@ int fer_gemm(const fer_gemm_desc* d, const fer_epilogue* e, fer_stream_t stream)
  * (default) or 224 (678 instead of 591 tiles at 50,432 rows: 2.65 instead of 2.31 rounds of 256 CUs). */
 int fer_gemm_set_row_tile(int rows);
 /* Split-K GEMMs on the BK = 32 ring kernel (the MN x MN weight gradients dW = dY^T X of ViT-B's linears,
- * `image_vit.py:101-113` backward) with an fp32-output epilogue: 1 (default) = the K splits are summed
- * inside the launch by the last split of each tile (tile tickets), 0 = a separate reduction launch.
- * Both add the splits in split order: bit-identical results. */
+ * `image_vit.py:101-113` backward) with an fp32-output epilogue: 1 = the K splits are summed inside the
+ * launch by the last split of each tile (tile tickets), 0 (default, measured faster) = a separate
+ * reduction launch. Both add the splits in split order: bit-identical results. */
 int fer_gemm_set_splitk_fold(int on);
 
 /* Grouped weight gradients: dw[n][k] (+)= sum_m dy[m][n] x[m][k] (bf16 dy [M][N] row stride ld_dy,

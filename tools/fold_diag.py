@@ -27,7 +27,7 @@ def main():
         ops.linear_wgrad(dy, x, c)
         torch.cuda.synchronize()
         outs.append(c)
-    lib().fer_gemm_set_splitk_fold(1)
+    lib().fer_gemm_set_splitk_fold(0)
     ws = [b for k, b in ops.WS.buf.items() if k[1] == 1][0]
     S = 6
     slab = ws[: S * N * K].view(S, N, K)

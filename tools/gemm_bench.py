@@ -104,7 +104,7 @@ def main():
             if tf is not None:
                 ref[k].append(timeit(tf))
     lib().fer_gemm_set_row_tile(256)
-    lib().fer_gemm_set_splitk_fold(1)
+    lib().fer_gemm_set_splitk_fold(0)
     tag = cfg if cfg is not None else "auto"
     for k, (fn, fl, tf) in cases.items():
         for rt, _ in rows:

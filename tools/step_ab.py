@@ -100,7 +100,7 @@ def main():
         lib().fer_attention_set_fwd_kernel(0)
         lib().fer_gemm_set_config(-1)
         lib().fer_gemm_set_row_tile(256)
-        lib().fer_gemm_set_splitk_fold(1)
+        lib().fer_gemm_set_splitk_fold(0)
         opt.step_in_backward(False)
         opt.cache_table = True
         runtime.WGRAD.enabled = True
