@@ -11,8 +11,8 @@ gfx940+, and the address not at all). Measured here (profi
     v_lshl_add_u64 four slots later: one 8-row pass of a tile left unwritten about once in 40 launches.
 The pass walks each store's following instructions in program order; when a VALU (v_*) or an LDS read writes one of
 the store's registers less than W slots after it, an s_nop of the missing slots goes in front of that
-instruction. A window that reaches a label or branch first is padded there (the successor is not
-followed). Every other instruction is left as it is.
+instruction, on every path: branches are followed into their targets (both successors of a conditional
+branch). Every other instruction is left as it is.
 
     python store_hazard_pad.py in.s out.s [W]
 """
@@ -80,29 +80,48 @@ def nops(n, indent="\t"):
 
 
 def pad(lines, W):
+    """Pads in front of every VALU / LDS-read write of a store's register on any path that reaches it
+    less than W slots after the store: branches are followed into their targets (both ways for a
+    conditional one), so a window that leaves a block is padded only where an overwrite happens."""
+    labels = {}
+    for i, l in enumerate(lines):
+        m = LABEL.match(l.strip())
+        if m:
+            labels[l.strip()[:-1]] = i
     insert_before = {}  # line index -> slots to pad in front of it
+
+    def walk(j, used, live, seen):
+        while j < len(lines) and used < W:
+            t = lines[j]
+            s_ = t.strip()
+            if not is_instr(t):
+                j += 1
+                continue
+            if valu_dst(t) & live:
+                insert_before[j] = max(insert_before.get(j, 0), W - used)
+                return
+            if BRANCH.match(t):
+                op = s_.split()[0]
+                if op.startswith("s_endpgm") or op.startswith(("s_setpc", "s_swappc")):
+                    return
+                target = s_.split()[1] if len(s_.split()) > 1 else None
+                used += slots(t)
+                if target in labels and (target, used) not in seen:
+                    seen.add((target, used))
+                    walk(labels[target] + 1, used, live, seen)
+                if op == "s_branch":
+                    return
+                j += 1
+                continue
+            used += slots(t)
+            j += 1
+
     for i, l in enumerate(lines):
         if not STORE.match(l):
             continue
         live = store_regs(l)
-        if not live:
-            continue
-        used = 0
-        for j in range(i + 1, len(lines)):
-            t = lines[j]
-            if LABEL.match(t.strip()) or BRANCH.match(t):
-                if used < W:
-                    insert_before[j] = max(insert_before.get(j, 0), W - used)
-                break
-            if not is_instr(t):
-                continue
-            if valu_dst(t) & live:
-                if used < W:
-                    insert_before[j] = max(insert_before.get(j, 0), W - used)
-                break
-            used += slots(t)
-            if used >= W:
-                break
+        if live:
+            walk(i + 1, 0, live, set())
     out = []
     for i, l in enumerate(lines):
         if i in insert_before:

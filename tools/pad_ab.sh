@@ -12,7 +12,7 @@ for lib in libfervit.so libfervit_nopad.so; do
   FERVIT_LIB=$L/$lib GD_STRESS=${REPS:-150} timeout -k 10 400 python -u tools/gemm_determinism.py 2>&1 \
     | grep -v amdgpu.ids | sed "s/^/[$lib] /" | tee -a gpurun_out/${TAG}_stress.txt | tail -3 || exit 1
 done
-for rep in 1 2; do for lib in libfervit.so libfervit_nopad.so; do
+for rep in 1 2 3; do for lib in libfervit.so libfervit_nopad.so; do
   FERVIT_LIB=$L/$lib timeout -k 10 300 python -u bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-traffic \
     2>/dev/null | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('[$lib]', d['ms_per_step'], d['step_ms_median'], d['roofline']['frac'], d['roofline'].get('frac_in_step'))" \
     | tee -a gpurun_out/${TAG}_bench_ab.txt || exit 1
