@@ -71,6 +71,16 @@ for s in $STEPS; do
       timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "$KT" \
         > gpurun_out/${TAG}_ktest.txt 2>&1 || { tail -30 gpurun_out/${TAG}_ktest.txt; exit 1; }
       tail -5 gpurun_out/${TAG}_ktest.txt ;;
+    smoke)  # __graft_entry__.smoke() on cuda:0
+      timeout -k 10 300 python -u -c 'import __graft_entry__ as g; g.smoke()' > gpurun_out/${TAG}_smoke.txt 2>&1 \
+        || { tail -20 gpurun_out/${TAG}_smoke.txt; exit 1; }
+      tail -3 gpurun_out/${TAG}_smoke.txt ;;
+    configs)  # the other bench configurations (SURVEY 8(d) cfg 2, 4, 5 and the 48 px ImageViT)
+      for c in latent_vit hybrid_latent_vit expression_aware_vit image_vit_48; do
+        timeout -k 10 300 python -u bench.py --config $c --steps ${CFG_STEPS:-50} --warmup 10 --no-cpu-baseline \
+          > gpurun_out/${TAG}_bench_$c.json 2> gpurun_out/${TAG}_bench_$c.err || { tail -20 gpurun_out/${TAG}_bench_$c.err; exit 1; }
+        cut -c1-240 gpurun_out/${TAG}_bench_$c.json
+      done ;;
     determ)  # run-to-run and 256- vs 224-row bit equality of the residual-kind GEMM
       timeout -k 10 200 python -u tools/gemm_determinism.py > gpurun_out/${TAG}_determinism.txt 2>&1 \
         || { tail -20 gpurun_out/${TAG}_determinism.txt; exit 1; }
