@@ -53,7 +53,10 @@ class StepGraph:
         # captured on the warm-up stream: the library's per-stream workspaces (ops.WS) sized by
         # the warm-up are the ones the captured launches use (no allocation under capture)
         side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.graph(g, stream=side):
+        # thread_local: a CUDA call from another thread during the capture (RCCL's watchdog querying
+        # its events under DDP) must not invalidate it -- with "global" it did, now and then
+        # (hipErrorStreamCaptureInvalidated in test_rccl_one_rank_step_graph, profiles/r05u_gpu_tests.txt)
+        with torch.cuda.graph(g, stream=side, capture_error_mode="thread_local"):
             check(lib().fer_step_advance(self.counter.data_ptr(), ops.stream()), "step_advance")
             self.out = self.step_fn()
         torch.cuda.current_stream().wait_stream(side)
