@@ -217,8 +217,8 @@ FER_DEV void epi8_t(const EpiArgs& e, long m, long n, f32x4& v0, f32x4& v1, f32x
 // stores them (pointer stores behind the row check in the shared staged loop -- buffer stores there
 // made the 128^2 kernel's STORE / MUL kinds 50-80 % slower on the latent shapes, profiles/r04z_* --
 // buffer stores with FER_OOB rows in the 8-phase kernel's register-fed and wave-private paths).
-template <int S0>
-FER_DEV bf16x8 epi8_k(const EpiArgs& e, uint32_t di, f32x4& v0, f32x4& v1, f32x4 b0, f32x4 b1, bf16x8 x,
+template <int S0, typename E>
+FER_DEV bf16x8 epi8_k(const E& e, uint32_t di, f32x4& v0, f32x4& v1, f32x4 b0, f32x4 b1, bf16x8 x,
                       uint64_t seed, float ab, f32x2 ghs, f32x2 gps, float dsr, bf16x8& gp) {
   constexpr int S = epi_base(S0);
   static_assert(S != EPI_GEN, "generic epilogue goes through epi8_t");
@@ -278,8 +278,8 @@ FER_DEV bf16x8 epi8_k(const EpiArgs& e, uint32_t di, f32x4& v0, f32x4& v1, f32x4
 }
 // epi8_k + buffer stores at byte offsets ocb / opb (FER_OOB for a row out of range: dropped without a
 // branch, so the compiler's wait counts around them stay exact)
-template <int S0>
-FER_DEV void epi8_kb(const EpiArgs& e, uint32_t ocb, uint32_t opb, uint32_t di, f32x4& v0, f32x4& v1, f32x4 b0,
+template <int S0, typename E>
+FER_DEV void epi8_kb(const E& e, uint32_t ocb, uint32_t opb, uint32_t di, f32x4& v0, f32x4& v1, f32x4 b0,
                      f32x4 b1, bf16x8 x, uint64_t seed, float ab, f32x2 ghs, f32x2 gps, float dsr,
                      const __amdgpu_buffer_rsrc_t& rc, const __amdgpu_buffer_rsrc_t& rp) {
   constexpr int S = epi_base(S0);
@@ -1634,9 +1634,30 @@ FER_DEV void tile_8ph(const GemmArgs& g, const EpiArgs& e, int bid, char* smem, 
 // alpha / bias read through the EpiArgs reference were kept in a per-thread copy the compiler
 // promoted to LDS, and that read waited vmcnt(0) for the LDS DMA -- r04ag.) The row-operand and
 // gate kinds stay on tile_8ph: this schedule for them (gpurun_out/patches/
-// gemm_pipelined_all_kinds.patch) faulted the GPU on its first residual launch (M 20000, N 3000,
-// K 520; profiles/r04af_pipelined_all_kinds_fault_ktests.txt), cause not found.
-constexpr int PP_SV = 16;
+// gemm_pipelined_all_kinds.patch) faulted the GPU (r04af, r05w): cause found in r05y -- in the second
+// tile on, a spilled SGPR pair reloaded by v_readlane right before the inline-asm claim atomic that
+// takes it as its address, without the 5 wait states "VALU writes SGPR -> VMEM reads it" needs (LLVM
+// does not look inside inline asm); the build pass (store_hazard_pad.py) now pads every such site.
+// The gate and row-operand kinds (FER_PP_KINDS=1, epilogue fields by value in PpEpiX) then pass the
+// kernel tests but measured slower (profiles/r05y_*: gate-mul +16 us, fc2 fwd +2-5 us, the step +0.3
+// ms), so they are built only on request (make EXTRA=-DFER_PP_KINDS=1).
+// PP_SV(EK): the vector-memory instructions every wave's epilogue issues after pro_8ph, all of them
+// unconditional (FER_OOB offsets): 16 output stores; GATE / GATER 16 pre-activation gate stores;
+// RES / MUL the row operand of chunks 2..7 (12 loads). Anything the compiler adds only makes the
+// next tile's first waits stricter; the epilogue's compiler barriers keep its loads from moving
+// above pro_8ph (which would make them looser).
+#ifndef FER_PP_KINDS
+#define FER_PP_KINDS 0
+#endif
+template <int EK>
+constexpr int pp_sv() {
+  constexpr int S = epi_base(EK);
+  return 16 + ((S == EPI_GATE || S == EPI_GATER) ? 16 : 0) + ((S == EPI_RES || S == EPI_MUL) ? 12 : 0);
+}
+template <int EK>
+constexpr bool pp_kind() {
+  return EK == EPI_STORE || (FER_PP_KINDS && (EK == EPI_GATE || EK == EPI_GATER || EK == EPI_RES2 || EK == EPI_MUL2));
+}
 
 // Always exactly ten instructions per wave, without a branch (the epilogue's compiler-placed waits
 // for its bias loads would otherwise merge the issue and no-issue paths into a
@@ -1715,15 +1736,127 @@ FER_DEV void epi_8ph_pp(const GemmArgs& g, const PpEpi& e, f32x4 (&acc)[4][8], c
   bar_lds();  // the staging area is K-tile 1's B units
 }
 
+// The pipelined schedule's epilogue for the gate and row-operand kinds: the staging of epi_8ph_pp
+// (eight 16-row chunks through the wave's 4 KB of stage 1's B units) feeding the fixed-kind
+// arithmetic of tile_epilogue_wp (epi8_kb, same operations in the same order, so bit-identical to
+// the plain schedule; the MUL column sums walk each lane's rows in the same ascending order). The
+// bias and the first two chunks' row operand are loaded before the next tile's prologue DMA, the
+// row operand of chunk c + 2 after chunk c's stores.
+struct PpEpiX {
+  void* c;
+  void* pre;
+  const void* x;  // row operand: res (RES) or aux (MUL)
+  const float* bias;
+  long ldc, ldp, ldx;
+  float alpha, drop_scale;
+  uint32_t drop_thresh, drop_ld;
+  uint64_t seed;
+};
+template <bool AKC, bool BKC, int MT, int EK>
+FER_DEV void epi_8ph_ppx(const GemmArgs& g, const PpEpiX& e, f32x4 (&acc)[4][8], char* smem, int m0, int n0,
+                         int wave, int lane, int next) {
+  constexpr int UNIT = 16384, BUF = 4 * UNIT;
+  constexpr int S = epi_base(EK);
+  constexpr bool X = S == EPI_RES || S == EPI_MUL;
+  constexpr bool CS = S == EPI_MUL;
+  const int wr = wave >> 2, wc = wave & 3;
+  const int prow = lane >> 3, pc = 8 * (lane & 7);
+  const int n = n0 + wc * 64 + pc;
+  const bool nok = n < g.N;  // N % 8 == 0 on this path (checked by the host)
+  const float dsc = e.drop_thresh ? e.drop_scale : 1.f;
+  const float ab = (S == EPI_RES || EK == EPI_GATER) ? e.alpha * dsc : e.alpha;
+  const f32x2 ghs = f32x2(0.5f * dsc), gps = f32x2(0.39894228040143268f * dsc);
+  const uint64_t seed = e.drop_thresh ? step_seed(e.seed) : 0;
+  const __amdgpu_buffer_rsrc_t rbias = make_rsrc(e.bias ? (const void*)e.bias : e.c);
+  const uint32_t boff = (e.bias && nok) ? (uint32_t)n * 4 : FER_OOB;
+  f32x4 b0 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rbias, boff, 0, 0));
+  f32x4 b1 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rbias, boff + 16, 0, 0));
+  const __amdgpu_buffer_rsrc_t rc = make_rsrc(e.c), rp = make_rsrc(e.pre ? e.pre : e.c);
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(X && e.x ? e.x : e.c);
+  const uint32_t ldcb = (uint32_t)e.ldc * 2, ldpb = (uint32_t)e.ldp * 2, ldxb = X ? (uint32_t)e.ldx * 2 : 0u;
+  const int rw0 = m0 + wr * 128 + prow;  // this lane's row in pass 0 of chunk 0
+  auto load_x = [&](int c, bf16x8 (&xc)[2]) {
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int row = rw0 + c * 16 + p * 8;
+      const uint32_t off = (nok && row < g.M) ? (uint32_t)row * ldxb + (uint32_t)n * 2 : FER_OOB;
+      xc[p] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rx, off, 0, 0));
+    }
+  };
+  bf16x8 xr[2][2];
+  if constexpr (X) {
+    load_x(0, xr[0]);
+    load_x(1, xr[1]);
+  }
+  asm volatile("" ::: "memory");
+  pro_8ph<AKC, BKC, MT, EK>(g, next, smem, wave, lane);
+  asm volatile("" ::: "memory");  // (the row-operand loads below stay younger than the DMA: PP_SV)
+  if (S == EPI_RES || EK == EPI_GATER) {
+    b0 *= dsc;
+    b1 *= dsc;
+  }
+  f32x4 cs0 = f32x4{0.f, 0.f, 0.f, 0.f}, cs1 = cs0;
+  char* const ws = smem + BUF + 2 * UNIT + wave * 4096;
+  auto swz = [](int row, int c16) { return row * 256 + ((c16 ^ row) << 4); };
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) *(f32x4*)(ws + swz(lane & 15, 4 * i + (lane >> 4))) = acc[i][c];
+    // (a wave's own LDS accesses complete in order: no barrier)
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int lrow = p * 8 + prow;
+      f32x4 v0 = *(const f32x4*)(ws + swz(lrow, pc >> 2)), v1 = *(const f32x4*)(ws + swz(lrow, (pc >> 2) + 1));
+      const int row = rw0 + c * 16 + p * 8;
+      const bool ok = nok && row < g.M;
+      const uint32_t di = (uint32_t)row * e.drop_ld + (uint32_t)n;
+      epi8_kb<EK>(e, ok ? (uint32_t)row * ldcb + (uint32_t)n * 2 : FER_OOB,
+                  ok ? (uint32_t)row * ldpb + (uint32_t)n * 2 : FER_OOB, di, v0, v1, b0, b1,
+                  X ? xr[c & 1][p] : bf16x8{}, seed, ab, ghs, gps, dsc, rc, rp);
+      if constexpr (CS) {
+        cs0 += ok ? v0 : f32x4{0.f, 0.f, 0.f, 0.f};
+        cs1 += ok ? v1 : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+    if constexpr (X) {
+      if (c + 2 < 8) load_x(c + 2, xr[c & 1]);
+    }
+  }
+  if constexpr (CS) {
+    if (g.cs_part) {
+      // over the 8 row lanes of the column group (lanes 8 apart), fixed order
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+#pragma unroll
+        for (int d = 8; d < 64; d <<= 1) {
+          cs0[r] += __shfl_xor(cs0[r], d);
+          cs1[r] += __shfl_xor(cs1[r], d);
+        }
+      }
+      float* red = (float*)(smem + BUF + 2 * UNIT);  // [2 wave-row halves][256 columns]
+      bar_lds();                                     // every wave is done with its staging
+      if (prow == 0) {
+        *(f32x4*)(red + wr * 256 + wc * 64 + pc) = cs0;
+        *(f32x4*)(red + wr * 256 + wc * 64 + pc + 4) = cs1;
+      }
+      bar_lds();
+      const int t = threadIdx.x;
+      if (t < 256 && n0 + t < g.N) g.cs_part[(long)(m0 / 256) * g.N + n0 + t] = red[t] + red[256 + t];
+    }
+  }
+  bar_lds();  // the staging area is K-tile 1's B units
+}
+
 // One tile of the pipelined schedule; returns the workgroup's next tile (-1: none). PEND: the
 // previous tile's epilogue sits between this tile's prologue DMA and its first wait (every tile
 // but a workgroup's first; a template flag: as a loop-carried bool it took a VGPR that spilled).
-template <bool AKC, bool BKC, int MT, int EK, bool PEND>
-FER_DEV int tile_8ph_pp(const GemmArgs& g, const PpEpi& e, int bid, char* smem, lds_vint* slot) {
-  static_assert(MT == 16 && EK == EPI_STORE, "pipelined schedule: MT 16 fragments, plain kind");
+template <bool AKC, bool BKC, int MT, int EK, bool PEND, typename EP>
+FER_DEV int tile_8ph_pp(const GemmArgs& g, const EP& e, int bid, char* smem, lds_vint* slot) {
+  static_assert(MT == 16 && pp_kind<EK>(), "pipelined schedule: MT 16 fragments, the pipelined kinds");
   constexpr int UNIT = 16384, BUF = 4 * UNIT;
   constexpr int FM = 8, FN = 4, QJ = 4, QI = 2, KS = 2;
-  constexpr int SV = PP_SV;
+  constexpr int SV = pp_sv<EK>();
+  static_assert(6 + SV <= 63, "vmcnt range");
   int tid = threadIdx.x;
   asm volatile("" : "+v"(tid));
   const int lane = tid & 63;
@@ -1841,7 +1974,10 @@ FER_DEV int tile_8ph_pp(const GemmArgs& g, const PpEpi& e, int bid, char* smem, 
     if (next >= g.tiles_m * g.tiles_n) next = -1;
   }
 
-  epi_8ph_pp<AKC, BKC, MT>(g, e, acc, smem, m0, n0, wave, lane, next);
+  if constexpr (EK == EPI_STORE)
+    epi_8ph_pp<AKC, BKC, MT>(g, e, acc, smem, m0, n0, wave, lane, next);
+  else
+    epi_8ph_ppx<AKC, BKC, MT, EK>(g, e, acc, smem, m0, n0, wave, lane, next);
   return next;
 }
 
@@ -1857,7 +1993,7 @@ template <bool AKC, bool BKC, int MT, bool DYN, int EK, int HR = 128>
 __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmArgs g, EpiArgs e) {
   __shared__ __attribute__((aligned(1024))) char smem[8 * 16384 + 16];
   const int ntiles = g.tiles_m * g.tiles_n;
-  if constexpr (EK == EPI_STORE && MT == 16) {
+  if constexpr (MT == 16 && HR == 128 && pp_kind<EK>()) {
     lds_vint* slot = DYN ? FER_LDS_INT(smem + 8 * 16384) : nullptr;
     int bid = DYN ? wq_first(ntiles) : ((int)blockIdx.x < ntiles ? (int)blockIdx.x : -1);
     if (bid < 0) return;
@@ -1866,10 +2002,17 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmArgs g, EpiArgs e)
       asm volatile("" : "+v"(tid));
       pro_8ph<AKC, BKC, MT, EK>(g, bid, smem, __builtin_amdgcn_readfirstlane(tid >> 6), tid & 63);
     }
-    const PpEpi pe{e.c, e.bias, (long)e.ldc, e.alpha};
-    bid = tile_8ph_pp<AKC, BKC, MT, EK, false>(g, pe, bid, smem, slot);
+    auto run = [&](const auto& pe) {
+      bid = tile_8ph_pp<AKC, BKC, MT, EK, false>(g, pe, bid, smem, slot);
 #pragma unroll 1
-    while (bid >= 0) bid = tile_8ph_pp<AKC, BKC, MT, EK, true>(g, pe, bid, smem, slot);
+      while (bid >= 0) bid = tile_8ph_pp<AKC, BKC, MT, EK, true>(g, pe, bid, smem, slot);
+    };
+    if constexpr (EK == EPI_STORE) {
+      run(PpEpi{e.c, e.bias, (long)e.ldc, e.alpha});
+    } else {
+      run(PpEpiX{e.c, e.pre, e.res ? e.res : e.aux, e.bias, (long)e.ldc, (long)e.ldp, (long)(e.res ? e.ldr : e.ldx),
+                 e.alpha, e.drop_scale, e.drop_thresh, (uint32_t)e.drop_ld, e.seed});
+    }
   } else if constexpr (!DYN) {
 #pragma unroll 1
     for (int bid = blockIdx.x; bid < ntiles; bid += gridDim.x) {

@@ -14,6 +14,15 @@ the store's registers less than W slots after it, an s_nop of the missing slots 
 instruction, on every path: branches are followed into their targets (both successors of a conditional
 branch). Every other instruction is left as it is.
 
+The same pass also pads inline assembly against "VALU writes SGPR -> VMEM reads that SGPR" (5 wait
+states on gfx9 / CDNA): LLVM's hazard recognizer does not look at inline-asm operands, and a
+v_readlane_b32 reloading a spilled SGPR right before the work-queue claim (an inline-asm
+global_atomic_add whose 64-bit address is an SGPR pair) let the atomic read the pair's old value:
+the round-4 / round-5 GPU faults of the pipelined GEMM schedule (DESIGN.md section 10,
+profiles/r05w_*, tools/check_asm_sgpr_hazard.py). Every inline-asm vector-memory instruction that
+reads an SGPR gets an s_nop in front of it when a VALU instruction writing that SGPR is fewer than 5
+wait states before it, or when a label (another block's path) comes first.
+
     python store_hazard_pad.py in.s out.s [W]
 """
 import re
@@ -130,15 +139,70 @@ def pad(lines, W):
     return out, len(insert_before)
 
 
+VMEM = re.compile(r"^\s*(global|buffer|flat|scratch)_\w+")
+SREG = re.compile(r"\bs\[(\d+):(\d+)\]|\bs(\d+)\b")
+SGPR_WS = 5  # VALU writes SGPR -> VMEM reads that SGPR
+
+
+def sregs(text):
+    out = set()
+    for m in SREG.finditer(text):
+        if m.group(3):
+            out.add(int(m.group(3)))
+        else:
+            out.update(range(int(m.group(1)), int(m.group(2)) + 1))
+    return out
+
+
+def valu_sdst(line):
+    t = line.strip()
+    if not t.startswith("v_"):
+        return set()
+    parts = t.split(None, 1)
+    return sregs(parts[1].split(",")[0]) if len(parts) > 1 else set()
+
+
+def pad_asm_sgpr(lines):
+    """s_nop in front of every inline-asm VMEM instruction that reads an SGPR written by a VALU
+    instruction fewer than SGPR_WS wait states earlier (or with a label within that window)."""
+    out, n, inasm = [], 0, False
+    for i, l in enumerate(lines):
+        t = l.strip()
+        if t.startswith(";;#ASMSTART"):
+            inasm = True
+        elif t.startswith(";;#ASMEND"):
+            inasm = False
+        elif inasm and VMEM.match(l):
+            need = sregs(t.split(None, 1)[1]) if len(t.split(None, 1)) > 1 else set()
+            used, j, short = 0, i - 1, 0
+            while need and j >= 0 and used < SGPR_WS:
+                tj = lines[j].strip()
+                if LABEL.match(tj):
+                    short = SGPR_WS - used  # another path may reach here: assume the worst
+                    break
+                if is_instr(lines[j]):
+                    if valu_sdst(lines[j]) & need:
+                        short = SGPR_WS - used
+                        break
+                    used += slots(lines[j])
+                j -= 1
+            if short > 0:
+                out.append(f"\ts_nop {short - 1}\t; inline-asm SGPR read hazard pad\n")
+                n += 1
+        out.append(l)
+    return out, n
+
+
 def main():
     src, dst = sys.argv[1], sys.argv[2]
     W = int(sys.argv[3]) if len(sys.argv) > 3 else W_DEFAULT
     with open(src) as f:
         lines = f.readlines()
     out, n = pad(lines, W)
+    out, na = pad_asm_sgpr(out)
     with open(dst, "w") as f:
         f.writelines(out)
-    print(f"store_hazard_pad: {n} pads ({W} slots) in {src}", file=sys.stderr)
+    print(f"store_hazard_pad: {n} pads ({W} slots), {na} inline-asm SGPR pads in {src}", file=sys.stderr)
 
 
 if __name__ == "__main__":

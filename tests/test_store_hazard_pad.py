@@ -84,3 +84,68 @@ def test_branch_targets_followed():
     assert nop_slots_before(out, "v_mov_b32_e32 v1, 0") == 15
     assert nop_slots_before(out, "v_mov_b32_e32 v2, 0") == 13
     assert n == 2
+
+
+def test_inline_asm_sgpr_read_after_valu_write_padded():
+    # the round-4 / round-5 fault: a spilled SGPR reloaded by v_readlane right before the inline-asm
+    # claim atomic that takes the pair as its address
+    lines = [l + "\n" for l in """
+\tv_readlane_b32 s6, v255, 3
+\tv_mov_b32_e32 v0, 1
+\tv_readlane_b32 s7, v255, 4
+\t;;#ASMSTART
+\tglobal_atomic_add v243, v194, v0, s[6:7] sc0
+\t;;#ASMEND
+\ts_mov_b32 s8, s9
+\t;;#ASMSTART
+\tglobal_atomic_add v243, v194, v0, s[8:9] sc0
+\t;;#ASMEND
+""".strip("\n").split("\n")]
+    out, n = shp.pad_asm_sgpr(lines)
+    out = [l.rstrip("\n") for l in out]
+    assert n == 1
+    i = next(k for k, l in enumerate(out) if "s[6:7]" in l)
+    assert out[i - 1].strip().startswith("s_nop 4")  # the full 5 wait states in front of the atomic
+    # an SGPR written by SALU needs no pad
+    j = next(k for k, l in enumerate(out) if "s[8:9]" in l)
+    assert "s_nop" not in out[j - 1]
+
+
+def test_inline_asm_sgpr_pad_counts_wait_states_and_labels():
+    lines = [l + "\n" for l in """
+\tv_readfirstlane_b32 s5, v1
+\ts_nop 1
+\tv_mov_b32_e32 v2, 0
+\t;;#ASMSTART
+\tbuffer_load_dwordx4 v3, s[8:11], s5 offen lds
+\t;;#ASMEND
+.LBB0_1:
+\t;;#ASMSTART
+\tbuffer_load_dwordx4 v3, s[8:11], 0 offen lds
+\t;;#ASMEND
+""".strip("\n").split("\n")]
+    out, n = shp.pad_asm_sgpr(lines)
+    out = [l.rstrip("\n") for l in out]
+    assert n == 2
+    i = next(k for k, l in enumerate(out) if "s5 offen" in l)
+    assert out[i - 1].strip().startswith("s_nop 1")  # 3 slots there (s_nop 1 + v_mov): 2 more
+    j = next(k for k, l in enumerate(out) if ", 0 offen lds" in l)
+    assert out[j - 1].strip().startswith("s_nop 4")  # a label right before: assume the worst
+
+
+def test_built_assembly_has_no_inline_asm_sgpr_hazard():
+    """The assembly the library is built from (csrc/build/*.pad.s, present after build()) has no
+    inline-asm vector-memory instruction reading a VALU-written SGPR within 5 wait states."""
+    import glob
+
+    import pytest
+
+    files = glob.glob(os.path.join(ROOT, "fer-vit_amd", "csrc", "build", "*.pad.s"))
+    if not files:
+        pytest.skip("library not built in this tree")
+    spec2 = importlib.util.spec_from_file_location("check_asm_sgpr_hazard",
+                                                   os.path.join(ROOT, "tools", "check_asm_sgpr_hazard.py"))
+    chk = importlib.util.module_from_spec(spec2)
+    spec2.loader.exec_module(chk)
+    for f in files:
+        assert chk.scan(f) == [], f
