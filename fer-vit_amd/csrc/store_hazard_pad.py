@@ -25,6 +25,7 @@ wait states before it, or when a label (another block's path) comes first.
 
     python store_hazard_pad.py in.s out.s [W]
 """
+import os
 import re
 import sys
 
@@ -199,7 +200,9 @@ def main():
     with open(src) as f:
         lines = f.readlines()
     out, n = pad(lines, W)
-    out, na = pad_asm_sgpr(out)
+    na = 0
+    if os.environ.get("PAD_SGPR", "1") != "0":  # (PAD_SGPR=0: A/B builds only)
+        out, na = pad_asm_sgpr(out)
     with open(dst, "w") as f:
         f.writelines(out)
     print(f"store_hazard_pad: {n} pads ({W} slots), {na} inline-asm SGPR pads in {src}", file=sys.stderr)

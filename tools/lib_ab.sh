@@ -1,7 +1,7 @@
 # One GPU call: a build A/B. The in-tree library (fer-vit_amd/fervit/libfervit.so) against another
 # build in the same directory ($BASE, default libfervit_base.so): the GPU tests matching $KT on the
 # in-tree library, then interleaved GEMM microbenchmarks ($GB_ONLY cases) and short bench runs on both.
-# usage: [KT=...] [GB_ONLY=...] [BASE=lib.so] [REPS=3] bash tools/lib_ab.sh <tag> [tests] [gbench] [bench]
+# usage: [KT=...] [GB_ONLY=...] [BASE=lib.so] [REPS=3] [CFG=bench config] [BSTEPS=30] bash tools/lib_ab.sh <tag> [tests] [gbench] [bench]
 set -o pipefail
 TAG=${1:-ab}; shift
 STEPS=${*:-tests gbench bench}
@@ -21,8 +21,8 @@ for s in $STEPS; do
       done; done ;;
     bench)
       for rep in $(seq ${REPS:-3}); do for lib in $LIBS; do
-        FERVIT_LIB=$L/$lib timeout -k 10 300 python -u bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-traffic \
-          2>/dev/null | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('[$lib]', d['ms_per_step'], d['step_ms_median'], d['roofline']['frac'], d['roofline'].get('frac_in_step'))" \
+        FERVIT_LIB=$L/$lib timeout -k 10 300 python -u bench.py --config ${CFG:-vit_base_224} --steps ${BSTEPS:-30} --warmup 5 --no-cpu-baseline --no-traffic \
+          2>/dev/null | tail -1 | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('[$lib]', d['ms_per_step'], d['step_ms_median'], (d.get('roofline') or {}).get('frac'), (d.get('roofline') or {}).get('frac_in_step'))" \
           | tee -a gpurun_out/${TAG}_bench_ab.txt || exit 1
       done; done ;;
   esac
