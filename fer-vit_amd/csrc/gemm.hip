@@ -1642,21 +1642,23 @@ FER_DEV void tile_8ph(const GemmArgs& g, const EpiArgs& e, int bid, char* smem, 
 // kernel tests but measured slower (profiles/r05y_*: gate-mul +16 us, fc2 fwd +2-5 us, the step +0.3
 // ms), so they are built only on request (make EXTRA=-DFER_PP_KINDS=1).
 // PP_SV(EK): the vector-memory instructions every wave's epilogue issues after pro_8ph, all of them
-// unconditional (FER_OOB offsets): 16 output stores; GATE / GATER 16 pre-activation gate stores;
-// RES / MUL the row operand of chunks 2..7 (12 loads). Anything the compiler adds only makes the
-// next tile's first waits stricter; the epilogue's compiler barriers keep its loads from moving
-// above pro_8ph (which would make them looser).
+// unconditional (FER_OOB offsets): 16 output stores; GATE / GATER 16 pre-activation gate stores (the
+// row operand of RES / MUL is loaded before pro_8ph). Anything the compiler adds only makes the next
+// tile's first waits stricter; the epilogue's compiler barriers keep its memory operations on their
+// side of pro_8ph.
 #ifndef FER_PP_KINDS
 #define FER_PP_KINDS 0
 #endif
 template <int EK>
 constexpr int pp_sv() {
   constexpr int S = epi_base(EK);
-  return 16 + ((S == EPI_GATE || S == EPI_GATER) ? 16 : 0) + ((S == EPI_RES || S == EPI_MUL) ? 12 : 0);
+  return 16 + ((S == EPI_GATE || S == EPI_GATER) ? 16 : 0);
 }
+// FER_PP_KINDS bits: 1 the gate kinds (GATE, GATER), 2 RES2, 4 MUL2
 template <int EK>
 constexpr bool pp_kind() {
-  return EK == EPI_STORE || (FER_PP_KINDS && (EK == EPI_GATE || EK == EPI_GATER || EK == EPI_RES2 || EK == EPI_MUL2));
+  return EK == EPI_STORE || ((FER_PP_KINDS & 1) && (EK == EPI_GATE || EK == EPI_GATER)) ||
+         ((FER_PP_KINDS & 2) && EK == EPI_RES2) || ((FER_PP_KINDS & 4) && EK == EPI_MUL2);
 }
 
 // Always exactly ten instructions per wave, without a branch (the epilogue's compiler-placed waits
@@ -1740,8 +1742,7 @@ FER_DEV void epi_8ph_pp(const GemmArgs& g, const PpEpi& e, f32x4 (&acc)[4][8], c
 // (eight 16-row chunks through the wave's 4 KB of stage 1's B units) feeding the fixed-kind
 // arithmetic of tile_epilogue_wp (epi8_kb, same operations in the same order, so bit-identical to
 // the plain schedule; the MUL column sums walk each lane's rows in the same ascending order). The
-// bias and the first two chunks' row operand are loaded before the next tile's prologue DMA, the
-// row operand of chunk c + 2 after chunk c's stores.
+// bias and all eight chunks' row operand (64 VGPRs) are loaded before the next tile's prologue DMA.
 struct PpEpiX {
   void* c;
   void* pre;
@@ -1783,14 +1784,16 @@ FER_DEV void epi_8ph_ppx(const GemmArgs& g, const PpEpiX& e, f32x4 (&acc)[4][8],
       xc[p] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rx, off, 0, 0));
     }
   };
-  bf16x8 xr[2][2];
+  // every chunk's row operand before the next tile's prologue DMA: a load issued after the DMA would
+  // make the wait for it (in-order vmcnt) wait for the DMA and the earlier stores too
+  bf16x8 xr[8][2];
   if constexpr (X) {
-    load_x(0, xr[0]);
-    load_x(1, xr[1]);
+#pragma unroll
+    for (int c = 0; c < 8; ++c) load_x(c, xr[c]);
   }
   asm volatile("" ::: "memory");
   pro_8ph<AKC, BKC, MT, EK>(g, next, smem, wave, lane);
-  asm volatile("" ::: "memory");  // (the row-operand loads below stay younger than the DMA: PP_SV)
+  asm volatile("" ::: "memory");
   if (S == EPI_RES || EK == EPI_GATER) {
     b0 *= dsc;
     b1 *= dsc;
@@ -1812,14 +1815,11 @@ FER_DEV void epi_8ph_ppx(const GemmArgs& g, const PpEpiX& e, f32x4 (&acc)[4][8],
       const uint32_t di = (uint32_t)row * e.drop_ld + (uint32_t)n;
       epi8_kb<EK>(e, ok ? (uint32_t)row * ldcb + (uint32_t)n * 2 : FER_OOB,
                   ok ? (uint32_t)row * ldpb + (uint32_t)n * 2 : FER_OOB, di, v0, v1, b0, b1,
-                  X ? xr[c & 1][p] : bf16x8{}, seed, ab, ghs, gps, dsc, rc, rp);
+                  X ? xr[c][p] : bf16x8{}, seed, ab, ghs, gps, dsc, rc, rp);
       if constexpr (CS) {
         cs0 += ok ? v0 : f32x4{0.f, 0.f, 0.f, 0.f};
         cs1 += ok ? v1 : f32x4{0.f, 0.f, 0.f, 0.f};
       }
-    }
-    if constexpr (X) {
-      if (c + 2 < 8) load_x(c + 2, xr[c & 1]);
     }
   }
   if constexpr (CS) {
