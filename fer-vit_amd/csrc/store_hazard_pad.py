@@ -54,11 +54,15 @@ def store_regs(line):
     return regs(body)
 
 
+LDS_RET = re.compile(r"^ds_(read|load|bpermute|permute|swizzle)|^ds_\w*_rtn")
+
+
 def valu_dst(line):
-    """Registers written soon after issue: VALU destinations and LDS-load destinations (an LDS read
-    returns within tens of cycles; vector-memory loads return far later and are not tracked)."""
+    """Registers written soon after issue: VALU destinations and the destinations of LDS instructions
+    that return data (reads, ds_bpermute / ds_permute / ds_swizzle, returning atomics: tens of cycles);
+    vector-memory loads return far later and are not tracked."""
     t = line.strip()
-    if not (t.startswith("v_") or t.startswith("ds_read") or t.startswith("ds_load")):
+    if not (t.startswith("v_") or LDS_RET.match(t)):
         return set()
     parts = t.split(None, 1)
     if len(parts) < 2:

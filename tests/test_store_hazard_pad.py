@@ -149,3 +149,14 @@ def test_built_assembly_has_no_inline_asm_sgpr_hazard():
     spec2.loader.exec_module(chk)
     for f in files:
         assert chk.scan(f) == [], f
+
+
+def test_lds_returning_ops_tracked():
+    # a ds_bpermute writing a store's data register right after the store is padded like an LDS read
+    out, n = run("""
+\tbuffer_store_dword v5, v1, s[8:11], 0 offen
+\tds_bpermute_b32 v5, v2, v3
+\tbuffer_store_dword v6, v1, s[8:11], 0 offen
+\tds_write_b32 v6, v7
+""")
+    assert n == 1 and nop_slots_before(out, "ds_bpermute_b32") == 16
