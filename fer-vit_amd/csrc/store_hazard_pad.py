@@ -31,7 +31,8 @@ import sys
 
 W_DEFAULT = 16
 
-STORE = re.compile(r"^\s*(global|buffer|flat|scratch)_store_\w+")
+# vector-memory stores and atomics (an atomic reads its address and data registers the same way)
+STORE = re.compile(r"^\s*((global|buffer|flat|scratch)_store_\w+|(global|buffer|flat)_atomic_\w+)")
 BRANCH = re.compile(r"^\s*s_(branch|cbranch_\w+|setpc_b64|swappc_b64|endpgm\w*)\b")
 LABEL = re.compile(r"^[.\w$]+:")
 REG = re.compile(r"\b([va])(\d+)\b|\b([va])\[(\d+):(\d+)\]")

@@ -160,3 +160,11 @@ def test_lds_returning_ops_tracked():
 \tds_write_b32 v6, v7
 """)
     assert n == 1 and nop_slots_before(out, "ds_bpermute_b32") == 16
+
+
+def test_atomic_operands_tracked():
+    out, n = run("""
+\tglobal_atomic_add v235, v2, v3, s[56:57] sc0
+\tv_mov_b32_e32 v3, 0
+""")
+    assert n == 1 and nop_slots_before(out, "v_mov_b32_e32 v3, 0") == 16
