@@ -1,4 +1,5 @@
-"""Run one ViT-B GEMM a few times (PMC profiling target): GEMM_CASE=fc1|fc1_fused|wgrad."""
+"""Run one ViT-B GEMM a few times (PMC profiling target): GEMM_CASE=fc1 (K 768, plain) | fc2 (K 3072, plain) |
+fc1_fused (bias + GELU + dropout + pre)."""
 import os
 import sys
 
@@ -16,9 +17,15 @@ b = torch.zeros(F, device="cuda")
 pre = torch.empty(M, F, device="cuda", dtype=torch.bfloat16)
 out = torch.empty(M, F, device="cuda", dtype=torch.bfloat16)
 case = os.environ.get("GEMM_CASE", "fc1")
+if case == "fc2":
+    h = torch.randn(M, F, device="cuda", generator=g).to(torch.bfloat16)
+    w2 = (torch.randn(D, F, device="cuda", generator=g) * 0.03).to(torch.bfloat16)
+    y2 = torch.empty(M, D, device="cuda", dtype=torch.bfloat16)
 for _ in range(6):
     if case == "fc1":
         ops.linear_fwd(x, w, out=out)
+    elif case == "fc2":
+        ops.linear_fwd(h, w2, out=y2)
     else:
         ops.linear_fwd(x, w, b, out=out, pre=pre, act="gelu", dropout=0.1, seed=7)
 torch.cuda.synchronize()
