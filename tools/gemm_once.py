@@ -1,5 +1,5 @@
 """Run one ViT-B GEMM a few times (PMC profiling target): GEMM_CASE=fc1 (K 768, plain) | fc2 (K 3072, plain) |
-fc1_fused (bias + GELU + dropout + pre)."""
+fc1_fused (bias + GELU + dropout + pre). GEMM_CFG=<n>: force library config n (fer_gemm_set_config)."""
 import os
 import sys
 
@@ -8,6 +8,10 @@ sys.path.insert(0, os.path.join(ROOT, "fer-vit_amd"))
 import torch  # noqa: E402
 
 from fervit import ops  # noqa: E402
+from fervit._lib import lib  # noqa: E402
+
+if os.environ.get("GEMM_CFG"):
+    lib().fer_gemm_set_config(int(os.environ["GEMM_CFG"]))
 
 M, D, F = 256 * 197, 768, 3072
 g = torch.Generator(device="cuda").manual_seed(0)
