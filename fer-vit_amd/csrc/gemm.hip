@@ -1553,24 +1553,30 @@ FER_DEV void tile_8ph(const GemmArgs& g, const EpiArgs& e, int bid, char* smem, 
       const int st_i = 4 + (T * 4 + q) * 4;
       if (T < 16) FER_STAMP(st_i);
       // ---- load segment
+      // Fragment reads spread over the four phases (quadrants in the order (0,0) (0,1) (1,1) (1,0)):
+      // B0 in phase 0 (with A0 in the first K-tile), B1 in phase 1, A1 in phase 2 and the next K-tile's
+      // A0 in phase 3, 4-8 reads per load segment instead of 12, 12, 0, 0 (profiles/r05bf_*).
       if (q < 2) {
-        const char* ua = unit(T, q);
         const char* ub = unit(T, 2 + q);
 #pragma unroll
         for (int kk = 0; kk < KS; ++kk)
 #pragma unroll
           for (int i = 0; i < QI; ++i) fb[q][kk][i] = read_frag<MT, 128, BKC, 64>(ub, wc * 32 + i * MT, kk, lane);
+      }
+      if ((q == 0 && T == 0) || q == 2 || (q == 3 && n1)) {
+        const int qa = q == 2 ? 1 : 0;
+        const char* ua = unit(q == 3 ? T + 1 : T, qa);
 #pragma unroll
         for (int kk = 0; kk < KS; ++kk)
 #pragma unroll
-          for (int j = 0; j < QJ; ++j) fa[q][kk][j] = read_frag<MT, 128, AKC, 64>(ua, wr * 64 + j * MT, kk, lane);
+          for (int j = 0; j < QJ; ++j) fa[qa][kk][j] = read_frag<MT, 128, AKC, 64>(ua, wr * 64 + j * MT, kk, lane);
       }
       if (q == 0) {
         if (n1) { iB0(T + 1); wait_vm<4>(); } else { wait_vm<0>(); }
       } else if (q == 1) {
         if (n1) iA1(T + 1);
       } else if (q == 2) {
-        if (n1) iB1(T + 1);
+        if (n1) { iB1(T + 1); wait_vm<6>(); }  // the next K-tile's A0 (phase 3 reads it)
       } else {
         if (n2) { iA0(T + 2); wait_vm<6>(); } else if (n1) { wait_vm<4>(); }
       }
@@ -1578,11 +1584,11 @@ FER_DEV void tile_8ph(const GemmArgs& g, const EpiArgs& e, int bid, char* smem, 
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
       if (T < 16) FER_STAMP(st_i + 2);
-      // ---- MFMA segment: quadrant (qm, qn) for q = 0..3 -> (0,0) (1,1) (0,1) (1,0)
+      // ---- MFMA segment: quadrant (qm, qn) for q = 0..3 -> (0,0) (0,1) (1,1) (1,0)
       constexpr int dummy = 0;
       (void)dummy;
-      const int qm = (q == 0 || q == 2) ? 0 : 1;
-      const int qn = (q == 0 || q == 3) ? 0 : 1;
+      const int qm = q >= 2 ? 1 : 0;
+      const int qn = (q == 1 || q == 2) ? 1 : 0;
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int kk = 0; kk < KS; ++kk)
@@ -1915,17 +1921,23 @@ FER_DEV int tile_8ph_pp(const GemmArgs& g, const EP& e, int bid, char* smem, lds
     const bool n1 = T + 1 < nk, n2 = T + 2 < nk;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
+      // Fragment reads spread over the four phases (quadrants in the order (0,0) (0,1) (1,1) (1,0)):
+      // B0 in phase 0 (with A0 in the first K-tile), B1 in phase 1, A1 in phase 2 and the next K-tile's
+      // A0 in phase 3, 4-8 reads per load segment instead of 12, 12, 0, 0 (profiles/r05bf_*).
       if (q < 2) {
-        const char* ua = unit(T, q);
         const char* ub = unit(T, 2 + q);
 #pragma unroll
         for (int kk = 0; kk < KS; ++kk)
 #pragma unroll
           for (int i = 0; i < QI; ++i) fb[q][kk][i] = read_frag<MT, 128, BKC, 64>(ub, wc * 32 + i * MT, kk, lane);
+      }
+      if ((q == 0 && T == 0) || q == 2 || (q == 3 && n1)) {
+        const int qa = q == 2 ? 1 : 0;
+        const char* ua = unit(q == 3 ? T + 1 : T, qa);
 #pragma unroll
         for (int kk = 0; kk < KS; ++kk)
 #pragma unroll
-          for (int j = 0; j < QJ; ++j) fa[q][kk][j] = read_frag<MT, 128, AKC, 64>(ua, wr * 64 + j * MT, kk, lane);
+          for (int j = 0; j < QJ; ++j) fa[qa][kk][j] = read_frag<MT, 128, AKC, 64>(ua, wr * 64 + j * MT, kk, lane);
       }
       if (q == 0) {
         if (n1) {
@@ -1937,14 +1949,17 @@ FER_DEV int tile_8ph_pp(const GemmArgs& g, const EP& e, int bid, char* smem, lds
       } else if (q == 1) {
         if (n1) iA1(T + 1);
       } else if (q == 2) {
-        if (n1) iB1(T + 1);
+        if (n1) {  // the next K-tile's A0 (phase 3 reads it)
+          iB1(T + 1);
+          if (PEND && T == 0) wait_vm<6 + SV>(); else wait_vm<6>();
+        }
       } else {
         if (n2) { iA0(T + 2); wait_vm<6>(); } else if (n1) { wait_vm<4>(); }
       }
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
-      const int qm = (q == 0 || q == 2) ? 0 : 1;
-      const int qn = (q == 0 || q == 3) ? 0 : 1;
+      const int qm = q >= 2 ? 1 : 0;
+      const int qn = (q == 1 || q == 2) ? 1 : 0;
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int kk = 0; kk < KS; ++kk)
