@@ -55,6 +55,9 @@ extern "C" int fer_set_step_counter(const uint64_t* counter) {
 
 extern "C" int fer_stream_create_cu_mask(const uint32_t* mask, int nwords, int priority, fer_stream_t* out) {
   if (!out || nwords < 0 || (nwords > 0 && !mask)) return fer::set_error("stream_create_cu_mask: bad arguments");
+  // hipExtStreamCreateWithCUMask has neither a priority nor a flags argument: refuse a priority it
+  // would silently drop (the masked stream is created blocking, at the default priority)
+  if (nwords > 0 && priority != 0) return fer::set_error("stream_create_cu_mask: priority must be 0 with a CU mask");
   hipStream_t s = nullptr;
   hipError_t e = nwords == 0 ? hipStreamCreateWithPriority(&s, hipStreamNonBlocking, priority)
                              : hipExtStreamCreateWithCUMask(&s, (uint32_t)nwords, mask);

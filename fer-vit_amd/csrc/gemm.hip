@@ -1623,6 +1623,120 @@ FER_DEV void tile_8ph(const GemmArgs& g, const EpiArgs& e, int bid, char* smem, 
 #endif
 }
 
+// ---- Ring ping-pong main loop (round 6). Same 256x256 tile, wave split (2 row halves x 4 column
+// quarters, 128 x 64 per wave, MFMA 16x16x32) and epilogues as tile_8ph, but the K loop runs BK = 32
+// stages through a 4-slot LDS ring (4 x 32 KB: A [256][32] + B [256][32] per slot) with ONE load
+// segment and ONE 32-MFMA segment per wave and K-step:
+//   LOAD(t):  12 ds_read_b128 of slot t (8 A + 4 B fragments), LDS-DMA of stage t+3 (4 pieces per
+//             wave), counted vmcnt for stage t+1, lgkmcnt(0), s_barrier
+//   MFMA(t):  32 MFMAs (s_setprio 1), s_barrier
+// with waves 4-7 one barrier behind waves 0-3, so every SIMD pairs one wave's MFMA segment with its
+// partner's load segment. Per 64 of K: 4 barrier intervals of 32 MFMAs per SIMD instead of the 8-phase
+// loop's 8 of 16, the same fragment-read and DMA density per MFMA, and each stage issued three K-steps
+// (about five intervals) before its first read instead of two to three phases.
+// Slot (t+3)%4 = (t-1)%4 is refilled in LOAD(t): the other group read it in its LOAD(t-1), which ended
+// with lgkmcnt(0) before the barrier that precedes this LOAD(t). Stage t+1: each wave waits for its own
+// pieces in LOAD(t); the barrier after LOAD(t) of the later group publishes all of them before the
+// earlier group's LOAD(t+1).
+template <bool AKC, bool BKC, int EK, int NST = 4>
+FER_DEV void tile_rpp(const GemmArgs& g, const EpiArgs& e, int bid, char* smem, lds_vint* claim_slot) {
+  constexpr int MT = 16, RBK = 32, PD = NST - 1;  // PD: stages in flight ahead of the one being read
+  constexpr int A_BYTES = 256 * RBK * 2, STAGE = 2 * A_BYTES;
+  typedef DmaPlan<256, AKC, 8, MT, RBK> PA;
+  typedef DmaPlan<256, BKC, 8, MT, RBK> PB;
+  static_assert(PA::NI + PB::NI == 4, "four DMA pieces per wave and stage");
+  int tid = threadIdx.x;
+  asm volatile("" : "+v"(tid));
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  int tm, tn;
+  tile_of(bid, g.tiles_m, g.tiles_n, tm, tn, EK == EPI_GATE ? 4 : 8);
+  const int m0 = tm * 256, n0 = tn * 256;
+  const int kbeg = (int)blockIdx.y * g.k_chunk;
+  const int kend = min(g.K, kbeg + g.k_chunk);
+  const int nk = (kend - kbeg + RBK - 1) / RBK;
+  const int ktail = kbeg + (nk - 1) * RBK;
+  const u32x4 ra = rsrc4(g.A), rb = rsrc4(g.B);
+  PA pa;
+  PB pb;
+  pa.init(wave, lane, g.lda, m0, g.M);
+  pb.init(wave, lane, g.ldb, n0, g.N);
+  auto slot = [&](int t) -> char* { return smem + (NST == 4 ? (t & 3) : t % NST) * STAGE; };
+  auto issue = [&](int t) {
+    const int k0 = kbeg + t * RBK;
+    pa.issue(ra, slot(t), wave, g.lda, k0, kend, k0 == ktail);
+    pb.issue(rb, slot(t) + A_BYTES, wave, g.ldb, k0, kend, k0 == ktail);
+  };
+  // counted waits: stage s landed while the n younger stages may fly (4 pieces per stage and wave)
+  auto wait_stages = [](int n) {
+    if (n >= 3) wait_vm<12>();
+    else if (n == 2) wait_vm<8>();
+    else if (n == 1) wait_vm<4>();
+    else wait_vm<0>();
+  };
+  f32x4 acc[4][8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // the next tile's claim: issued ahead of the prologue DMA, retired by the prologue's counted wait
+  uint32_t craw = 0;
+  if (claim_slot && tid == 0) craw = wq_claim_issue(g.tq);
+  if (nk > 0) {
+#pragma unroll
+    for (int s = 0; s < PD; ++s)
+      if (s < nk) issue(s);
+    wait_stages(min(nk, PD) - 1);
+    __builtin_amdgcn_s_barrier();
+    if (wr) __builtin_amdgcn_s_barrier();  // stagger: waves 4-7 one barrier behind
+    asm volatile("" ::: "memory");
+  } else {
+    wait_vm<0>();
+  }
+  if (claim_slot && tid == 0) {
+    asm volatile("" : "+v"(craw));
+    *claim_slot = wq_claim_finish(craw, g.tq_base, g.tiles_m * g.tiles_n);
+  }
+
+#pragma unroll 1
+  for (int t = 0; t < nk; ++t) {
+    // ---- load segment
+    const char* cur = slot(t);
+    bf16x8 fa[8], fb[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) fb[i] = read_frag<MT, 256, BKC, RBK>(cur + A_BYTES, wc * 64 + i * MT, 0, lane);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) fa[j] = read_frag<MT, 256, AKC, RBK>(cur, wr * 128 + j * MT, 0, lane);
+    if (t + PD < nk) {
+      issue(t + PD);
+      wait_stages(PD - 1);  // stage t+1 (own pieces): stages t+2 .. t+PD may fly
+    } else if (t + 1 < nk) {
+      wait_stages(nk - t - 2);
+    }
+    bar_lds();  // own fragment reads complete; stage t+1 published to the other group
+    __builtin_amdgcn_sched_barrier(0);
+    // ---- MFMA segment
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[i][j] = mfma<MT>(fb[i], fa[j], acc[i][j]);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  }
+  if (nk > 0 && !wr) __builtin_amdgcn_s_barrier();  // waves 0-3 catch up with the stagger
+  if constexpr (EK != EPI_GEN)
+    tile_epilogue_wp<EK>(g, e, acc, smem, m0, n0, wr, wc, lane);
+  else
+    tile_epilogue<256, 256, 2, 4, MT, 2, 4 * STAGE, EK>(g, e, acc, smem, m0, n0, (int)blockIdx.y, wr, wc, lane);
+}
+// (NST = 5: five 32 KB stages = all 160 KB of the CU's LDS, no room for the work-queue hand-off word:
+// fixed stride only)
+
 // ---- Pipelined schedule for the plain kind (EPI_STORE, MT 16): a tile's epilogue overlaps the next
 // tile's first operand loads and its own store drain overlaps the next tile's first K-tile.
 // vmcnt retires in issue order, so in the plain schedule (epilogue stores, then the next tile's
@@ -2047,6 +2161,31 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmArgs g, EpiArgs e)
   }
 }
 
+// Persistent launch of the ring ping-pong main loop (tile_rpp), walking tiles as gemm_8ph_kernel does.
+template <bool AKC, bool BKC, bool DYN, int EK, int NST = 4>
+__global__ __launch_bounds__(512, 1) void gemm_rpp_kernel(GemmArgs g, EpiArgs e) {
+  static_assert(NST == 4 || !DYN, "the work-queue word needs LDS beyond the ring");
+  __shared__ __attribute__((aligned(1024))) char smem[NST == 4 ? 8 * 16384 + 16 : NST * 32768];
+  const int ntiles = g.tiles_m * g.tiles_n;
+  if constexpr (!DYN) {
+#pragma unroll 1
+    for (int bid = blockIdx.x; bid < ntiles; bid += gridDim.x) {
+      tile_rpp<AKC, BKC, EK, NST>(g, e, bid, smem, nullptr);
+      bar_lds();  // every wave is done with the epilogue's LDS before the next tile's DMA
+    }
+  } else {
+    lds_vint* slot = FER_LDS_INT(smem + 8 * 16384);
+    int bid = wq_first(ntiles), par = 0;
+#pragma unroll 1
+    while (bid >= 0) {
+      tile_rpp<AKC, BKC, EK>(g, e, bid, smem, slot + par);
+      bar_lds();  // every wave is done with the epilogue's LDS before the next tile's DMA
+      bid = __builtin_amdgcn_readfirstlane(slot[par]);
+      par ^= 1;
+    }
+  }
+}
+
 // Ordered (deterministic) split-K reduction + epilogue.
 template <typename T>
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ ws, int splits, long M, long N,
@@ -2311,6 +2450,12 @@ static int launch_ring(GemmArgs g, const EpiArgs& e, hipStream_t st) {
 }
 
 static int g_row_tile = 256;  // fer_gemm_set_row_tile
+// main loop of the 256^2 persistent kernel: 0 the 8-phase loop, 1 the ring ping-pong loop (tile_rpp);
+// fer_gemm_set_main_loop, FERVIT_GEMM_LOOP at start-up
+static int g_loop = [] {
+  const char* s = getenv("FERVIT_GEMM_LOOP");
+  return s ? atoi(s) : 0;
+}();
 
 template <bool AKC, bool BKC, int MT>
 static int launch_8ph(GemmArgs g, const EpiArgs& e, hipStream_t st) {
@@ -2332,7 +2477,7 @@ static int launch_8ph(GemmArgs g, const EpiArgs& e, hipStream_t st) {
   const int gx = std::min(ntiles, std::max(8, ncu / 8 * 8));
   g.tq = nullptr;
   WqArgs w{};
-  if (!fixed_stride_mode() && g.splits == 1) {
+  if (!fixed_stride_mode() && g.splits == 1 && !(MT == 16 && g_loop == 2)) {  // (loop 2: fixed stride)
     w = wq_prepare_here(st, gx, ntiles);
     g.tq = w.q;
     for (int c = 0; c < 8; ++c) g.tq_base[c] = w.base[c];
@@ -2351,6 +2496,47 @@ static int launch_8ph(GemmArgs g, const EpiArgs& e, hipStream_t st) {
     }                                                  \
   } else {                                             \
     FER_8PH(DY, EPI_GEN);                              \
+  }
+  if (MT == 16 && g_loop == 2 && !r224) {  // five-stage ring ping-pong, fixed stride (experiment)
+    g.tq = nullptr;
+    if constexpr (AKC && BKC) {
+      switch (ek) {
+        case EPI_STORE: hipLaunchKernelGGL((gemm_rpp_kernel<AKC, BKC, false, EPI_STORE, 5>), grid, dim3(512), 0, st, g, e); break;
+        case EPI_GATE: hipLaunchKernelGGL((gemm_rpp_kernel<AKC, BKC, false, EPI_GATE, 5>), grid, dim3(512), 0, st, g, e); break;
+        case EPI_RES2: hipLaunchKernelGGL((gemm_rpp_kernel<AKC, BKC, false, EPI_RES2, 5>), grid, dim3(512), 0, st, g, e); break;
+        case EPI_MUL2: hipLaunchKernelGGL((gemm_rpp_kernel<AKC, BKC, false, EPI_MUL2, 5>), grid, dim3(512), 0, st, g, e); break;
+        default: hipLaunchKernelGGL((gemm_rpp_kernel<AKC, BKC, false, EPI_GEN, 5>), grid, dim3(512), 0, st, g, e); break;
+      }
+    } else {
+      hipLaunchKernelGGL((gemm_rpp_kernel<AKC, BKC, false, EPI_GEN, 5>), grid, dim3(512), 0, st, g, e);
+    }
+    wq_check_launch(st, w);
+    return 0;
+  }
+  if (MT == 16 && g_loop == 1 && !r224) {  // ring ping-pong main loop (fer_gemm_set_main_loop)
+#define FER_RPP(DY, K) hipLaunchKernelGGL((gemm_rpp_kernel<AKC, BKC, DY, K>), grid, dim3(512), 0, st, g, e)
+#define FER_RPP_K(DY)                                  \
+  if constexpr (AKC && BKC) {                          \
+    switch (ek) {                                      \
+      case EPI_STORE: FER_RPP(DY, EPI_STORE); break;   \
+      case EPI_GATE: FER_RPP(DY, EPI_GATE); break;     \
+      case EPI_GATER: FER_RPP(DY, EPI_GATER); break;   \
+      case EPI_RES2: FER_RPP(DY, EPI_RES2); break;     \
+      case EPI_MUL2: FER_RPP(DY, EPI_MUL2); break;     \
+      default: FER_RPP(DY, EPI_GEN); break;            \
+    }                                                  \
+  } else {                                             \
+    FER_RPP(DY, EPI_GEN);                              \
+  }
+    if (g.tq) {
+      FER_RPP_K(true)
+    } else {
+      FER_RPP_K(false)
+    }
+#undef FER_RPP_K
+#undef FER_RPP
+    wq_check_launch(st, w);
+    return 0;
   }
   if constexpr (AKC && BKC && MT == 16) {
     if (r224) {
@@ -2657,6 +2843,11 @@ extern "C" int fer_gemm_set_splitk_fold(int on) {
   return 0;
 }
 
+extern "C" int fer_gemm_set_main_loop(int loop) {
+  if (loop < 0 || loop > 2) return fer::set_error("gemm_set_main_loop: 0 (8-phase), 1 (ring ping-pong), 2 (its 5-stage form)");
+  fer::g_loop = loop;
+  return 0;
+}
 extern "C" int fer_gemm_set_row_tile(int rows) {
   if (rows != 256 && rows != 224) return fer::set_error("gemm_set_row_tile: 256 or 224");
   fer::g_row_tile = rows;

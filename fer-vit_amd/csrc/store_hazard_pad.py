@@ -49,14 +49,24 @@ def regs(text):
     return out
 
 
-def store_regs(line):
-    """Registers a store reads: every v/a register among its operands (data and address)."""
+def store_regs(line, cls="all"):
+    """Registers a store reads: every v/a register among its operands (data and address). cls (PAD_CLASS,
+    experiment builds only): "data" = only the data operand (the first one of a store, the second of an
+    atomic), "addr" = only the rest."""
     body = line.split(None, 1)[1] if len(line.split(None, 1)) > 1 else ""
     body = body.split("//")[0].split(";")[0]
-    return regs(body)
+    if cls == "all":
+        return regs(body)
+    ops = [o.strip() for o in body.split(",")]
+    di = 1 if "atomic" in line.split(None, 1)[0] else 0
+    data = regs(ops[di]) if len(ops) > di else set()
+    return data if cls == "data" else regs(body) - data
 
 
 LDS_RET = re.compile(r"^ds_(read|load|bpermute|permute|swizzle)|^ds_\w*_rtn")
+
+
+WRITER = os.environ.get("PAD_WRITER", "")  # experiment builds only: pad only writers with this prefix
 
 
 def valu_dst(line):
@@ -65,6 +75,8 @@ def valu_dst(line):
     vector-memory loads return far later and are not tracked."""
     t = line.strip()
     if not (t.startswith("v_") or LDS_RET.match(t)):
+        return set()
+    if WRITER and not t.startswith(WRITER):
         return set()
     parts = t.split(None, 1)
     if len(parts) < 2:
@@ -135,7 +147,7 @@ def pad(lines, W):
     for i, l in enumerate(lines):
         if not STORE.match(l):
             continue
-        live = store_regs(l)
+        live = store_regs(l, os.environ.get("PAD_CLASS", "all"))
         if live:
             walk(i + 1, 0, live, set())
     out = []

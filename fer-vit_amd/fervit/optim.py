@@ -34,7 +34,7 @@ class FusedAdamW(torch.optim.Optimizer):
         # stream-ordered launch per step) -- no per-step pinned allocation and H2D copy. Re-uploaded
         # when the segment set or any hyper-parameter changes.
         self.cache_table = True
-        self._eager = None  # (device table, nseg, maxn, signature, counter)
+        self._eager = None  # (device table, nseg, maxn, signature, counter, host steps of its last launch)
         # step_in_backward(): per-layer updates issued from the backward's gradient-ready hook
         self._inbw = False
         self._bw_done = set()     # ids of parameters already updated in the current backward
@@ -117,6 +117,7 @@ class FusedAdamW(torch.optim.Optimizer):
         into the same device table before the next replay (sync_graph_hparams)."""
         flat = self._bind()
         self._eager = None
+        self._bw_tables = {}
         segs, maxn = self._segments(flat, bump=False)
         self._frozen = (self._upload(segs, flat), len(segs), maxn)
         # group of every segment (same walk as _segments), to rebuild the table with new hparams
@@ -154,7 +155,10 @@ class FusedAdamW(torch.optim.Optimizer):
         flat = self._bind()
         if not flat.data.is_cuda:
             return
-        ps = [p for p in params if id(p) in self._pgroup and p.grad is not None and id(p) not in self._bw_done]
+        if any(id(p) in self._bw_done for p in params if id(p) in self._pgroup and p.grad is not None):
+            raise RuntimeError("FusedAdamW.step_in_backward: a second backward reached parameters already updated "
+                               "since the last step() (gradient accumulation is not supported in this mode)")
+        ps = [p for p in params if id(p) in self._pgroup and p.grad is not None]
         if not ps:
             return
         segs, maxn = [], 0
@@ -170,18 +174,22 @@ class FusedAdamW(torch.optim.Optimizer):
             maxn = max(maxn, p.numel())
         key = tuple(id(p) for p in ps)
         sig = tuple(x[:7] for x in segs)
+        steps = tuple(x[7] for x in segs)
         e = self._bw_tables.get(key)
-        advance = e is not None and e[3] == sig
+        # reuse the resident table only if every parameter's host step moved by exactly one since the
+        # table's last launch (its device step = table step + counter advances by one per reuse);
+        # anything else -- another update path, a different subset, graph replays -- rebuilds it
+        advance = e is not None and e[3] == sig and all(s == t + 1 for s, t in zip(steps, e[7]))
         if not advance:
             dev = self._upload(segs, flat)
             counter = torch.zeros(1, dtype=torch.int64, device=flat.data.device)
             tsegs, tiles = flat.half_t_segments(ps)
-            e = (dev, len(segs), maxn, sig, counter, tsegs, tiles)
-            self._bw_tables[key] = e
-        dev, nseg, maxn, _, counter, tsegs, tiles = e
+            e = (dev, len(segs), maxn, sig, counter, tsegs, tiles, steps)
+        dev, nseg, maxn, _, counter, tsegs, tiles, _ = e
         if tsegs is None and flat.half_t is not None:  # the transposed copies appeared after the table was built
             tsegs, tiles = flat.half_t_segments(ps)
-            self._bw_tables[key] = e[:5] + (tsegs, tiles)
+        self._bw_tables[key] = (dev, nseg, maxn, sig, counter, tsegs, tiles, steps)
+        self._eager = None  # these parameters' steps moved outside step()'s resident table
         half = flat.bf16()
 
         def launch():
@@ -237,6 +245,7 @@ class FusedAdamW(torch.optim.Optimizer):
         self._frozen = None
         self._step_counter = None
         self._eager = None
+        self._bw_tables = {}
 
     def _segments(self, flat, bump: bool):
         segs = []
@@ -300,17 +309,20 @@ class FusedAdamW(torch.optim.Optimizer):
             return loss
         counter = None
         sig = tuple(s[:7] for s in segs)
+        steps = tuple(s[7] for s in segs)
         e = self._eager
-        if self.cache_table and e is not None and e[3] == sig and flat.data.is_cuda:
+        if (self.cache_table and e is not None and e[3] == sig and flat.data.is_cuda
+                and all(s == t + 1 for s, t in zip(steps, e[5]))):
             # same segments and hyper-parameters as the resident table, every step bumped by one since
             dev, counter = e[0], e[4]
             check(lib().fer_step_advance(counter.data_ptr(), ops.stream()), "adamw step")
+            self._eager = e[:5] + (steps,)
         else:
             dev = self._upload(segs, flat)
             self._eager = None
             if self.cache_table and flat.data.is_cuda:
                 counter = torch.zeros(1, dtype=torch.int64, device=flat.data.device)
-                self._eager = (dev, len(segs), maxn, sig, counter)
+                self._eager = (dev, len(segs), maxn, sig, counter, steps)
         self._segs_dev = dev
         half = flat.bf16()
         check(lib().fer_adamw(flat.data.data_ptr(), flat.grad.data_ptr(), self._m.data_ptr(), self._v.data_ptr(),
@@ -321,6 +333,7 @@ class FusedAdamW(torch.optim.Optimizer):
 
     def _step_subset(self, flat, params) -> None:
         """One eager update of `params` only (the ones step_in_backward's hook did not reach)."""
+        self._eager = None  # steps move outside the resident table (the per-layer tables check theirs)
         ids = {id(p) for p in params}
         segs, maxn = [], 0
         for g in self.param_groups:

@@ -265,9 +265,13 @@ class _WgradStream:
         self.enabled = True
         self.in_capture = False
         # CU mask of the side stream (list of 32-bit words, bit i = CU i; None: every CU). Set before
-        # the first backward; the stream is created on first use (fer_stream_create_cu_mask).
+        # the first backward; the stream is created on first use (fer_stream_create_cu_mask). A masked
+        # stream is a BLOCKING stream (hipExtStreamCreateWithCUMask takes no flags): beside work on the
+        # legacy null stream it serialises with it, so run the step on a non-blocking stream when a mask
+        # is set (tools/step_ab.py does).
         self.cu_mask: Optional[List[int]] = None
         self._handles = {}
+        self._retired = []  # masked handles of earlier reset()s, never destroyed (see reset)
 
     def _make(self, dev):
         if not self.cu_mask:
@@ -284,14 +288,16 @@ class _WgradStream:
         return torch.cuda.ExternalStream(h.value, device=dev)
 
     def reset(self):
-        """Drop the side streams (e.g. after changing cu_mask); call with no backward in flight."""
+        """Drop the side streams (e.g. after changing cu_mask); call with no backward in flight.
+
+        A CU-masked stream's handle is NOT destroyed: tensors such as flat.grad carry it from
+        record_stream(), and the caching allocator records an event on it whenever such a tensor is
+        freed, however much later -- on a destroyed handle that is an invalid-handle error or a
+        silently reused one. The handles stay alive for the life of the process (_retired)."""
         if self.streams:
             torch.cuda.synchronize()
         self.streams = {}
-        from ._lib import lib
-
-        for h in self._handles.values():
-            lib().fer_stream_destroy(h)
+        self._retired.extend(self._handles.values())
         self._handles = {}
 
     def _off(self) -> bool:

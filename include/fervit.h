@@ -80,6 +80,11 @@ int fer_gemm(const fer_gemm_desc* d, const fer_epilogue* e, fer_stream_t stream)
  * out_proj / linear2 forward and linear1 / in_proj input gradients, `image_vit.py:101-113`): 256
  * (default) or 224 (678 instead of 591 tiles at 50,432 rows: 2.65 instead of 2.31 rounds of 256 CUs). */
 int fer_gemm_set_row_tile(int rows);
+/* Main loop of the persistent 256 x 256 GEMM (every forward / input-gradient linear of
+ * `image_vit.py:101-113`): 0 (default) the 8-phase loop (BK 64, two LDS stages, 16-MFMA segments),
+ * 1 the ring ping-pong loop (BK 32, four LDS stages, 32-MFMA segments). Same results to rounding of
+ * the K order (both accumulate K in ascending order per accumulator: bit-identical). */
+int fer_gemm_set_main_loop(int loop);
 /* Split-K GEMMs on the BK = 32 ring kernel (the MN x MN weight gradients dW = dY^T X of ViT-B's linears,
  * `image_vit.py:101-113` backward) with an fp32-output epilogue: 1 = the K splits are summed inside the
  * launch by the last split of each tile (tile tickets), 0 (default, measured faster) = a separate
@@ -120,7 +125,10 @@ int fer_set_persistent_mode(int mode);
  * the driver's CU numbering; hipExtStreamCreateWithCUMask), or with nwords = 0 an unmasked stream
  * of the given priority. For the weight-gradient side stream of the backward
  * (`train/train_image_vit.py:124` loss.backward(): this path's dgrad / wgrad split over streams);
- * the caller owns the stream (fer_stream_destroy). */
+ * the caller owns the stream (fer_stream_destroy). With a mask the stream is a BLOCKING stream
+ * (it serialises with the legacy null stream) at the default priority, and a non-zero priority is
+ * an error; without one it is non-blocking. Destroy a stream only once no live tensor of the
+ * caller's allocator has it recorded (torch record_stream). */
 int fer_stream_create_cu_mask(const uint32_t* mask, int nwords, int priority, fer_stream_t* out);
 int fer_stream_destroy(fer_stream_t stream);
 

@@ -815,3 +815,59 @@ def test_wgrad_splitk_fold_bit_exact(M, N, K, acc):
     assert not bad, "; ".join(bad)
     ref = dy.float().t() @ x.float() + (c0 if acc else 0)
     assert rel_err(outs[1], ref) < 1e-3
+
+
+@pytest.mark.parametrize("M,N,K", [(1100, 520, 200), (20000, 3000, 520), (25600, 768, 768), (9000, 2048, 40),
+                                   (4000, 768, 3072)])
+@pytest.mark.parametrize("p", [0.0, 0.1])
+@pytest.mark.parametrize("loop", [1, 2])
+def test_gemm_main_loop_ring_pingpong(M, N, K, p, loop):
+    """The ring ping-pong main loop of the persistent 256x256 kernel (fer_gemm_set_main_loop(1): BK 32, four
+    LDS stages, one 32-MFMA segment per wave and K-step) against the 8-phase loop (0) on the same calls: every
+    fixed epilogue kind (plain, GELU gate, residual, gate multiply with column sums), the generic epilogue with
+    an MN-contiguous B operand (dgrad), ragged M / N and K tails -- bit-identical (both accumulate each output
+    in ascending K order), every element written (NaN prefill), and within bf16 tolerance of fp32 torch."""
+    from fervit._lib import lib
+
+    o = ops()
+    g = torch.Generator(device=DEV).manual_seed(M + N + K)
+    x = torch.randn(M, K, device=DEV, generator=g).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV, generator=g) / math.sqrt(K)).to(torch.bfloat16)
+    b = torch.randn(N, device=DEV, generator=g)
+    res = torch.randn(M, N, device=DEV, generator=g).to(torch.bfloat16)
+    dy = torch.randn(M, K, device=DEV, generator=g).to(torch.bfloat16)
+    w2 = (torch.randn(K, N, device=DEV, generator=g) / math.sqrt(N)).to(torch.bfloat16)  # [out=K, in=N]
+    nan = lambda *s: torch.full(s, float("nan"), device=DEV, dtype=torch.bfloat16)
+
+    def run():
+        out = {}
+        out["plain"] = o.linear_fwd(x, w, b, out=nan(M, N))
+        gate = nan(M, N)
+        out["gelu"] = o.linear_fwd(x, w, b, out=nan(M, N), pre=gate, pre_gate=True, act="gelu", dropout=p, seed=5)
+        out["gate"] = gate
+        out["res"] = o.linear_fwd(x, w, b, out=nan(M, N), res=res, dropout=p, seed=6)
+        cs = torch.zeros(N, device=DEV)
+        out["mul"] = o.linear_fwd(x, w, out=nan(M, N), aux=gate, aux_act="mul", colsum=cs)
+        out["mul_cs"] = cs
+        out["dgrad"] = o.linear_dgrad(dy, w2, out=nan(M, N))
+        torch.cuda.synchronize()
+        return out
+
+    lib().fer_gemm_set_config(8)
+    try:
+        lib().fer_gemm_set_main_loop(0)
+        a = run()
+        assert lib().fer_gemm_set_main_loop(loop) == 0
+        bb = run()
+        cc = run()
+    finally:
+        lib().fer_gemm_set_main_loop(0)
+        lib().fer_gemm_set_config(-1)
+    for k in a:
+        assert torch.isfinite(bb[k].float()).all(), k
+        assert torch.equal(a[k].view(torch.int16) if a[k].dtype == torch.bfloat16 else a[k],
+                           bb[k].view(torch.int16) if bb[k].dtype == torch.bfloat16 else bb[k]), k
+        assert torch.equal(bb[k], cc[k]), k
+    ref = x.float() @ w.float().t() + b
+    assert rel_err(bb["plain"], ref) < 1e-2
+    assert rel_err(bb["dgrad"], dy.float() @ w2.float()) < 1e-2

@@ -343,3 +343,71 @@ def test_step_in_backward_equals_step(prec):
     if a[4] is not None:
         assert all(torch.equal(u.view(torch.int16), v.view(torch.int16)) for u, v in zip(a[4], b[4]))
     assert a[5] == b[5]
+
+
+@pytest.mark.parametrize("pattern", [(True, False, True, True, False, True), (False, True, False, False, True, True)])
+def test_step_in_backward_switched_mid_run(pattern):
+    """step_in_backward switched on and off between steps (as tools/step_ab.py does between variants) ==
+    plain step() every step, bit for bit: the per-layer tables and step()'s resident table are reused only
+    when every parameter's host step moved by exactly one since their last launch, so a table
+    left stale by the other path is rebuilt instead of advanced with the wrong bias-correction step."""
+    import fervit
+    from fervit.loss import CrossEntropyLoss
+    from fervit.optim import FusedAdamW
+    from models_fer_vit.image_vit import ImageViT
+
+    g = torch.Generator().manual_seed(6)
+    x = torch.randn(16, 3, 48, 48, generator=g).to(DEV)
+    y = torch.randint(0, 7, (16,), generator=g).to(DEV)
+    crit = CrossEntropyLoss(label_smoothing=0.1)
+    out = []
+    for pat in ((False,) * len(pattern), pattern):
+        torch.manual_seed(0)
+        m = ImageViT(img_size=48, patch_size=16, embed_dim=384, depth=2, heads=8, mlp_dim=1536, dropout=0.1)
+        m = m.to(DEV).set_precision("bf16")
+        opt = FusedAdamW(m.parameters(), lr=1e-3, weight_decay=0.05, model=m)
+        fervit.manual_seed(12)
+        for inbw in pat:
+            opt.step_in_backward(inbw)
+            opt.zero_grad()
+            crit(m(x), y).backward()
+            opt.step()
+        opt.step_in_backward(False)
+        torch.cuda.synchronize()
+        out.append((m.fer_flat().data.clone(), opt._m.clone(), opt._v.clone(),
+                    [opt.state[p]["step"] for p in m.parameters()]))
+    a, b = out
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]) and torch.equal(a[2], b[2])
+    assert a[3] == b[3]
+
+
+def test_step_in_backward_second_backward_raises():
+    """Two backward passes before step() under step_in_backward (gradient accumulation) would apply only the
+    first pass's gradients to the parameters the hook already updated: refused with an error."""
+    from fervit.loss import CrossEntropyLoss
+    from fervit.optim import FusedAdamW
+    from models_fer_vit.image_vit import ImageViT
+
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(8, 3, 48, 48, generator=g).to(DEV)
+    y = torch.randint(0, 7, (8,), generator=g).to(DEV)
+    crit = CrossEntropyLoss()
+    m = ImageViT(img_size=48, patch_size=16, embed_dim=384, depth=1, heads=8, mlp_dim=1536, dropout=0.0)
+    m = m.to(DEV).set_precision("bf16")
+    opt = FusedAdamW(m.parameters(), lr=1e-3, model=m).step_in_backward(True)
+    try:
+        opt.zero_grad()
+        crit(m(x), y).backward()
+        with pytest.raises(RuntimeError, match="second backward"):
+            crit(m(x), y).backward()
+    finally:
+        from fervit import runtime
+        from fervit.optim import _close_reduce_window
+
+        opt.step_in_backward(False)
+        # the raising backward dropped its queued engine callbacks: join the weight-gradient stream and
+        # close the deferred-reduction window by hand so later tests start clean
+        runtime.WGRAD.join_queued = False
+        runtime.WGRAD.sync()
+        _close_reduce_window()
+        torch.cuda.synchronize()

@@ -88,6 +88,13 @@ def main():
 
     if os.environ.get("GB_ROWS") == "ab":
         rows = [("rows 256", lambda: lib().fer_gemm_set_row_tile(256)), ("rows 224", lambda: lib().fer_gemm_set_row_tile(224))]
+    elif os.environ.get("GB_LOOP") == "ab":  # main loop of the 256^2 kernel: 8-phase (0) vs ring ping-pong (1)
+        def setl(loop, fixed=0):
+            def f():
+                lib().fer_gemm_set_main_loop(loop)
+                lib().fer_set_persistent_mode(fixed)
+            return f
+        rows = [("loop 0", setl(0)), ("loop 1", setl(1)), ("loop 2 fixed", setl(2, 1)), ("loop 0 fixed", setl(0, 1))]
     elif os.environ.get("GB_FOLD") == "ab":
         rows = [("fold 1", lambda: lib().fer_gemm_set_splitk_fold(1)), ("fold 0", lambda: lib().fer_gemm_set_splitk_fold(0))]
     else:
@@ -105,6 +112,8 @@ def main():
                 ref[k].append(timeit(tf))
     lib().fer_gemm_set_row_tile(256)
     lib().fer_gemm_set_splitk_fold(0)
+    lib().fer_gemm_set_main_loop(0)
+    lib().fer_set_persistent_mode(0)
     tag = cfg if cfg is not None else "auto"
     for k, (fn, fl, tf) in cases.items():
         for rt, _ in rows:
