@@ -22,7 +22,6 @@ struct GemmArgs {
   float* cs_part;  // fused column sums: per-tile partials [tiles_m][N] (or null)
   int* tq;               // persistent 8-phase kernel: work-queue counters (common.h wq_*), null = fixed stride
   unsigned tq_base[8];   // their values at launch
-  unsigned* tick;        // split-K ring launches: per-tile tickets of the in-launch fold (null: splitk_reduce)
 };
 
 int set_error(const char* msg);

@@ -938,114 +938,6 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g, 
   tile_epilogue<BM, BN, WM, WN, MT, (BM >= 256 ? 2 : 1), SMEM, EK>(g, e, acc, smem, m0, n0, ks, wm, wn, lane);
 }
 
-// ---- split-K fold (ring launches, fer_gemm_set_splitk_fold): the reduction of the K splits inside
-// the GEMM launch instead of a separate splitk_reduce launch. Every split writes its partial tile to
-// the [split][M][N] fp32 slab with write-through (sc1) stores, drains them and takes a ticket from
-// the tile's counter (agent-scope atomic); the split that draws ticket S-1 reads the S slabs of the
-// tile in split order (sc1 loads, its own included), so the sum is p0 + p1 + ... + p(S-1) whatever
-// the arrival order -- the order splitk_reduce_kernel adds them in, hence bit-identical to it -- and
-// writes c (+)= alpha * sum (the weight-gradient epilogue: fp32 output, optional accumulate). It
-// then resets the counter to 0 for the next launch on its stream (no other split of the tile touches
-// it after the last ticket; the next launch is stream-ordered behind this one). The hand-off is the
-// grouped weight-gradient kernel's (gemm_wgrad_group_kernel, MI355X_MICROARCH.md workgroup
-// dispatch: sc1 stores / counter / acquire + sc1 loads at one workgroup per CU). Its c stores are
-// followed within three issue slots by packed-math writes of their data registers; built without
-// store_hazard_pad.py those stores wrote the new value of one dword in 4 lanes of 16 on every launch
-// (profiles/r05_store_war_fold_*).
-constexpr int FER_TICK_SLOTS = 16, FER_TICK_TILES = 256;
-static __device__ unsigned fer_tick[FER_TICK_SLOTS][FER_TICK_TILES];
-
-template <int BM, int BN, int WM, int WN, int MT, typename AccT, int FN, int FM>
-FER_DEV void splitk_fold(const GemmArgs& g, const EpiArgs& e, AccT (&acc)[FN][FM], char* smem, int tile, int m0,
-                         int n0, int ks, int wm, int wn, int lane) {
-  // whole tiles only (host: M % BM == N % BN == 0, slab and c under 2 GiB): one per-lane offset, the
-  // (split, block) part in the scalar offset
-  constexpr int TM = BM / WM, TN = BN / WN;
-  constexpr int NQ = MT == 32 ? 4 : 1;
-  const int lr = MT == 32 ? (lane & 31) : (lane & 15);
-  const int lc = MT == 32 ? 4 * (lane >> 5) : 4 * (lane >> 4);
-  const int S = g.splits;
-  const __amdgpu_buffer_rsrc_t rs = make_rsrc(g.ws);
-  const uint32_t lo = (uint32_t)(((m0 + wm * TM + lr) * g.N + n0 + wn * TN + lc) * 4);
-  auto so = [&](int sp, int i, int j, int q) -> int {  // element (j*MT, i*MT + 8q) of split sp
-    return __builtin_amdgcn_readfirstlane((int)((((long)sp * g.M + j * MT) * g.N + i * MT + 8 * q) * 4));
-  };
-#pragma unroll
-  for (int i = 0; i < FN; ++i)
-#pragma unroll
-    for (int j = 0; j < FM; ++j)
-#pragma unroll
-      for (int q = 0; q < NQ; ++q)
-        __builtin_amdgcn_raw_buffer_store_b128(
-            __builtin_bit_cast(u32x4, f32x4{acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]}),
-            rs, lo, so(ks, i, j, q), 16 /* sc1: write-through */);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's partial drained
-  __syncthreads();  // every wave's partial drained; every wave is past its last LDS read
-  lds_vuint* flag = FER_LDS_UINT(smem);
-  if (threadIdx.x == 0) {
-    const unsigned tk = __hip_atomic_fetch_add(g.tick + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (tk == (unsigned)(S - 1)) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(g.tick + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    *flag = tk;
-  }
-  __syncthreads();
-  if (*flag != (unsigned)(S - 1)) return;  // not the last split of this tile
-  // one accumulator column block (i) at a time -- its S slabs in split order, then c (+)= alpha * sum in
-  // epi4's order for an fp32 output with no other epilogue operand -- so only FM x NQ loaded pieces are
-  // live beside the accumulators (summing or writing the whole tile at once spilled)
-  const __amdgpu_buffer_rsrc_t rc = make_rsrc(e.c);
-  const uint32_t co = (uint32_t)(((long)(m0 + wm * TM + lr) * e.ldc + n0 + wn * TN + lc) * 4);
-#pragma unroll
-  for (int i = 0; i < FN; ++i) {
-    // two splits per round (2 x FM x NQ loads in flight): the reading split runs alone on its CU
-    // and its reads are latency-bound; the sum stays p0 + p1 + ... in split order
-#pragma unroll 1
-    for (int sp = 0; sp < S; sp += 2) {
-      const bool two = sp + 1 < S;
-      f32x4 v[FM][NQ], w[FM][NQ];
-#pragma unroll
-      for (int j = 0; j < FM; ++j)
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-          v[j][q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, lo, so(sp, i, j, q), 16));
-          w[j][q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, two ? lo : FER_OOB,
-                                                                                    so(sp + 1, i, j, q), 16));
-        }
-#pragma unroll
-      for (int j = 0; j < FM; ++j)
-#pragma unroll
-        for (int q = 0; q < NQ; ++q)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            float a = sp ? acc[i][j][4 * q + r] + v[j][q][r] : v[j][q][r];
-            acc[i][j][4 * q + r] = two ? a + w[j][q][r] : a;
-          }
-    }
-    f32x4 cv[FM][NQ];
-#pragma unroll
-    for (int j = 0; j < FM; ++j)
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        const int cs = __builtin_amdgcn_readfirstlane((int)(((long)j * MT * e.ldc + i * MT + 8 * q) * 4));
-        cv[j][q] = e.accumulate ? __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rc, co, cs, 0))
-                                : f32x4{0.f, 0.f, 0.f, 0.f};
-      }
-#pragma unroll
-    for (int j = 0; j < FM; ++j)
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        const int cs = __builtin_amdgcn_readfirstlane((int)(((long)j * MT * e.ldc + i * MT + 8 * q) * 4));
-        f32x4 v = f32x4{acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]};
-        v *= e.alpha;
-        if (e.accumulate) v += cv[j][q];
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rc, co, cs, 0);
-      }
-  }
-}
-
 // Ring variant: BK=32 stages in an NST-slot LDS ring, LDS-DMA issued NST-1 K-steps ahead and
 // spread over the substeps (so no wave blocks on a burst of DMA issue and each stage has
 // ~NST-2 K-steps to land). Per K-step t, in its last substep: counted vmcnt for stage t+1,
@@ -1171,13 +1063,6 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_ring_kernel(GemmArgs g, 
       for (int j = 0; j < FM; ++j) af[j] = an[j];
     }
   }
-  // (not in the 256^2 MT32 form, cfg 4: its 4 x 4-register row pieces per column block spill)
-  if constexpr (MT == 16 || BM < 256) {
-    if (g.tick) {
-      splitk_fold<BM, BN, WM, WN, MT>(g, e, acc, smem, tm * g.tiles_n + tn, m0, n0, ks, wm, wn, lane);
-      return;
-    }
-  }
   tile_epilogue<BM, BN, WM, WN, MT, EPC, NST * STAGE>(g, e, acc, smem, m0, n0, ks, wm, wn, lane);
 }
 
@@ -1294,13 +1179,13 @@ static int launch_pp(GemmArgs g, const EpiArgs& e, hipStream_t st) {
 // (each >= 3 phases after its last read in the same buffer). Waits: q=3 retires A0/B0(T+1)
 // (vmcnt 6: A1, B1(T+1), A0(T+2) may fly), q=0 retires A1/B1(T) (vmcnt 4); a unit is read one
 // phase after the wait that retires it (the barrier between publishes other waves' DMA).
-template <bool KC, int MT, bool ISA, int HR = 128>
+template <bool KC, int MT, bool ISA>
 struct UnitPlan {
   uint32_t base[2];
   int kof[2];
   // local index (0..127) -> index inside the 256-wide tile
   FER_DEV static int map(int l, int q) {
-    return ISA ? (l >> 6) * HR + q * 64 + (l & 63) : (l >> 5) * 64 + q * 32 + (l & 31);
+    return ISA ? (l >> 6) * 128 + q * 64 + (l & 63) : (l >> 5) * 64 + q * 32 + (l & 31);
   }
   FER_DEV void init(int wave, int lane, long ld, int r0, int rmax, int q) {
 #pragma unroll
@@ -1372,7 +1257,7 @@ FER_DEV unsigned long long stamp_now() {
 // instruction -- measured 10-25 % slower kernels: profiles/r04k_gemm_ab.txt.)
 // MUL's fused column sums (cs_part): per lane over its rows, over the 8 row lanes of a column group,
 // then the two wave-row halves through LDS.
-template <int EK, int HR = 128>
+template <int EK>
 FER_DEV void tile_epilogue_wp(const GemmArgs& g, const EpiArgs& e, f32x4 (&acc)[4][8], char* smem, int m0, int n0,
                               int wr, int wc, int lane) {
   constexpr int S = epi_base(EK);
@@ -1403,12 +1288,12 @@ FER_DEV void tile_epilogue_wp(const GemmArgs& g, const EpiArgs& e, f32x4 (&acc)[
   const __amdgpu_buffer_rsrc_t rx = make_rsrc(X && xs ? xs : e.c);
   const uint32_t ldcb = (uint32_t)e.ldc * 2, ldpb = (uint32_t)e.ldp * 2;
   const uint32_t ldxb = X ? (uint32_t)(e.res ? e.ldr : e.ldx) * 2 : 0u;
-  const int rw0 = m0 + wr * HR + prow;  // this lane's row in pass 0 of chunk 0
+  const int rw0 = m0 + wr * 128 + prow;  // this lane's row in pass 0 of chunk 0
   auto load_x = [&](int c, bf16x8 (&xc)[4]) {
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
       const int row = rw0 + c * 32 + p * 8;
-      const uint32_t off = (nok && row < g.M && (HR == 128 || c * 32 + p * 8 + prow < HR)) ? (uint32_t)row * ldxb + (uint32_t)n * 2 : FER_OOB;
+      const uint32_t off = (nok && row < g.M) ? (uint32_t)row * ldxb + (uint32_t)n * 2 : FER_OOB;
       xc[p] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rx, off, 0, 0));
     }
   };
@@ -1433,7 +1318,7 @@ FER_DEV void tile_epilogue_wp(const GemmArgs& g, const EpiArgs& e, f32x4 (&acc)[
       const int lrow = p * 8 + prow;
       f32x4 v0 = *(const f32x4*)(buf + swz(lrow, pc >> 2)), v1 = *(const f32x4*)(buf + swz(lrow, (pc >> 2) + 1));
       const int row = rw0 + c * 32 + p * 8;
-      const bool ok = nok && row < g.M && (HR == 128 || c * 32 + p * 8 + prow < HR);  // (HR < 128: the half's rows end at HR)
+      const bool ok = nok && row < g.M;
       const uint32_t di = (uint32_t)row * (uint32_t)e.drop_ld + (uint32_t)n;
       epi8_kb<EK>(e, ok ? (uint32_t)row * ldcb + (uint32_t)n * 2 : FER_OOB,
                   ok ? (uint32_t)row * ldpb + (uint32_t)n * 2 : FER_OOB, di, v0, v1, b0, b1,
@@ -1471,11 +1356,7 @@ FER_DEV void tile_epilogue_wp(const GemmArgs& g, const EpiArgs& e, f32x4 (&acc)[
 // claim_slot (work-queue mode): thread 0 claims a tile at the start of this one, before the
 // prologue's operand DMA, and parks the id in that LDS word after the prologue's wait (which
 // retires the atomic together with the previous tile's epilogue stores and the first K-tile)
-// HR: rows per wave-row half. 128 = the 256-row tile; 112 = a 224-row tile (N = 768 linears: 678 tiles = 2.65
-// rounds of 256 CUs instead of 591 = 2.31), whose A units still load 128 rows per half (the 16 rows past
-// the half are the other half's / the next tile's, read but never used) and whose quadrant-row 1 skips its
-// last 16-row MFMA block.
-template <bool AKC, bool BKC, int MT, int EK, int HR = 128>
+template <bool AKC, bool BKC, int MT, int EK>
 FER_DEV void tile_8ph(const GemmArgs& g, const EpiArgs& e, int bid, char* smem, lds_vint* claim_slot) {
   typedef typename Acc<MT>::T AccT;
   constexpr int UNIT = 16384, BUF = 4 * UNIT;  // A0 A1 B0 B1
@@ -1500,7 +1381,7 @@ FER_DEV void tile_8ph(const GemmArgs& g, const EpiArgs& e, int bid, char* smem, 
   // GELU-gate fc1 forward: row groups of 4 tiles (377 -> 367-370 us alone, profiles/r03w_tile_group_ab.txt;
   // the other kinds gain nothing from it)
   tile_of(bid, g.tiles_m, g.tiles_n, tm, tn, EK == EPI_GATE ? 4 : 8);
-  const int m0 = tm * (2 * HR), n0 = tn * 256;
+  const int m0 = tm * 256, n0 = tn * 256;
   const int ks = blockIdx.y;
   const int kbeg = ks * g.k_chunk;
   const int kend = min(g.K, kbeg + g.k_chunk);
@@ -1509,7 +1390,7 @@ FER_DEV void tile_8ph(const GemmArgs& g, const EpiArgs& e, int bid, char* smem, 
 
   const __amdgpu_buffer_rsrc_t ra = make_rsrc(g.A);
   const __amdgpu_buffer_rsrc_t rb = make_rsrc(g.B);
-  UnitPlan<AKC, MT, true, HR> pa0, pa1;
+  UnitPlan<AKC, MT, true> pa0, pa1;
   UnitPlan<BKC, MT, false> pb0, pb1;
   pa0.init(wave, lane, g.lda, m0, g.M, 0);
   pa1.init(wave, lane, g.lda, m0, g.M, 1);
@@ -1596,8 +1477,7 @@ FER_DEV void tile_8ph(const GemmArgs& g, const EpiArgs& e, int bid, char* smem, 
         for (int j = 0; j < QJ; ++j)
 #pragma unroll
           for (int i = 0; i < QI; ++i)
-            if (qm * QJ * MT + (j + 1) * MT <= HR)  // (HR < 128: the half's last rows carry no MFMA)
-              acc[qn * QI + i][qm * QJ + j] = mfma<MT>(fb[qn][kk][i], fa[qm][kk][j], acc[qn * QI + i][qm * QJ + j]);
+            acc[qn * QI + i][qm * QJ + j] = mfma<MT>(fb[qn][kk][i], fa[qm][kk][j], acc[qn * QI + i][qm * QJ + j]);
       __builtin_amdgcn_s_setprio(0);
       __builtin_amdgcn_sched_barrier(0);
       if (T < 16) FER_STAMP(st_i + 3);
@@ -1608,10 +1488,8 @@ FER_DEV void tile_8ph(const GemmArgs& g, const EpiArgs& e, int bid, char* smem, 
   if (nk > 0 && !wr) __builtin_amdgcn_s_barrier();  // waves 0-3 catch up with the stagger
   FER_STAMP(2);
   static_assert(64 * (256 + 4) * 4 <= 2 * BUF, "epilogue staging (2 chunks per half) must fit");
-  static_assert(HR == 128 || (EK != EPI_GEN && MT == 16 && epi_base(EK) != EPI_MUL),
-                "224-row tiles: wave-private epilogue kinds without column sums only");
   if constexpr (EK != EPI_GEN && MT == 16)
-    tile_epilogue_wp<EK, HR>(g, e, acc, smem, m0, n0, wr, wc, lane);
+    tile_epilogue_wp<EK>(g, e, acc, smem, m0, n0, wr, wc, lane);
   else
     tile_epilogue<256, 256, 2, 4, MT, 2, 2 * BUF, EK>(g, e, acc, smem, m0, n0, ks, wr, wc, lane);
   FER_STAMP(3);
@@ -1622,120 +1500,6 @@ FER_DEV void tile_8ph(const GemmArgs& g, const EpiArgs& e, int bid, char* smem, 
   }
 #endif
 }
-
-// ---- Ring ping-pong main loop (round 6). Same 256x256 tile, wave split (2 row halves x 4 column
-// quarters, 128 x 64 per wave, MFMA 16x16x32) and epilogues as tile_8ph, but the K loop runs BK = 32
-// stages through a 4-slot LDS ring (4 x 32 KB: A [256][32] + B [256][32] per slot) with ONE load
-// segment and ONE 32-MFMA segment per wave and K-step:
-//   LOAD(t):  12 ds_read_b128 of slot t (8 A + 4 B fragments), LDS-DMA of stage t+3 (4 pieces per
-//             wave), counted vmcnt for stage t+1, lgkmcnt(0), s_barrier
-//   MFMA(t):  32 MFMAs (s_setprio 1), s_barrier
-// with waves 4-7 one barrier behind waves 0-3, so every SIMD pairs one wave's MFMA segment with its
-// partner's load segment. Per 64 of K: 4 barrier intervals of 32 MFMAs per SIMD instead of the 8-phase
-// loop's 8 of 16, the same fragment-read and DMA density per MFMA, and each stage issued three K-steps
-// (about five intervals) before its first read instead of two to three phases.
-// Slot (t+3)%4 = (t-1)%4 is refilled in LOAD(t): the other group read it in its LOAD(t-1), which ended
-// with lgkmcnt(0) before the barrier that precedes this LOAD(t). Stage t+1: each wave waits for its own
-// pieces in LOAD(t); the barrier after LOAD(t) of the later group publishes all of them before the
-// earlier group's LOAD(t+1).
-template <bool AKC, bool BKC, int EK, int NST = 4>
-FER_DEV void tile_rpp(const GemmArgs& g, const EpiArgs& e, int bid, char* smem, lds_vint* claim_slot) {
-  constexpr int MT = 16, RBK = 32, PD = NST - 1;  // PD: stages in flight ahead of the one being read
-  constexpr int A_BYTES = 256 * RBK * 2, STAGE = 2 * A_BYTES;
-  typedef DmaPlan<256, AKC, 8, MT, RBK> PA;
-  typedef DmaPlan<256, BKC, 8, MT, RBK> PB;
-  static_assert(PA::NI + PB::NI == 4, "four DMA pieces per wave and stage");
-  int tid = threadIdx.x;
-  asm volatile("" : "+v"(tid));
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wave >> 2, wc = wave & 3;
-  int tm, tn;
-  tile_of(bid, g.tiles_m, g.tiles_n, tm, tn, EK == EPI_GATE ? 4 : 8);
-  const int m0 = tm * 256, n0 = tn * 256;
-  const int kbeg = (int)blockIdx.y * g.k_chunk;
-  const int kend = min(g.K, kbeg + g.k_chunk);
-  const int nk = (kend - kbeg + RBK - 1) / RBK;
-  const int ktail = kbeg + (nk - 1) * RBK;
-  const u32x4 ra = rsrc4(g.A), rb = rsrc4(g.B);
-  PA pa;
-  PB pb;
-  pa.init(wave, lane, g.lda, m0, g.M);
-  pb.init(wave, lane, g.ldb, n0, g.N);
-  auto slot = [&](int t) -> char* { return smem + (NST == 4 ? (t & 3) : t % NST) * STAGE; };
-  auto issue = [&](int t) {
-    const int k0 = kbeg + t * RBK;
-    pa.issue(ra, slot(t), wave, g.lda, k0, kend, k0 == ktail);
-    pb.issue(rb, slot(t) + A_BYTES, wave, g.ldb, k0, kend, k0 == ktail);
-  };
-  // counted waits: stage s landed while the n younger stages may fly (4 pieces per stage and wave)
-  auto wait_stages = [](int n) {
-    if (n >= 3) wait_vm<12>();
-    else if (n == 2) wait_vm<8>();
-    else if (n == 1) wait_vm<4>();
-    else wait_vm<0>();
-  };
-  f32x4 acc[4][8];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  // the next tile's claim: issued ahead of the prologue DMA, retired by the prologue's counted wait
-  uint32_t craw = 0;
-  if (claim_slot && tid == 0) craw = wq_claim_issue(g.tq);
-  if (nk > 0) {
-#pragma unroll
-    for (int s = 0; s < PD; ++s)
-      if (s < nk) issue(s);
-    wait_stages(min(nk, PD) - 1);
-    __builtin_amdgcn_s_barrier();
-    if (wr) __builtin_amdgcn_s_barrier();  // stagger: waves 4-7 one barrier behind
-    asm volatile("" ::: "memory");
-  } else {
-    wait_vm<0>();
-  }
-  if (claim_slot && tid == 0) {
-    asm volatile("" : "+v"(craw));
-    *claim_slot = wq_claim_finish(craw, g.tq_base, g.tiles_m * g.tiles_n);
-  }
-
-#pragma unroll 1
-  for (int t = 0; t < nk; ++t) {
-    // ---- load segment
-    const char* cur = slot(t);
-    bf16x8 fa[8], fb[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) fb[i] = read_frag<MT, 256, BKC, RBK>(cur + A_BYTES, wc * 64 + i * MT, 0, lane);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) fa[j] = read_frag<MT, 256, AKC, RBK>(cur, wr * 128 + j * MT, 0, lane);
-    if (t + PD < nk) {
-      issue(t + PD);
-      wait_stages(PD - 1);  // stage t+1 (own pieces): stages t+2 .. t+PD may fly
-    } else if (t + 1 < nk) {
-      wait_stages(nk - t - 2);
-    }
-    bar_lds();  // own fragment reads complete; stage t+1 published to the other group
-    __builtin_amdgcn_sched_barrier(0);
-    // ---- MFMA segment
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) acc[i][j] = mfma<MT>(fb[i], fa[j], acc[i][j]);
-    __builtin_amdgcn_s_setprio(0);
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-  }
-  if (nk > 0 && !wr) __builtin_amdgcn_s_barrier();  // waves 0-3 catch up with the stagger
-  if constexpr (EK != EPI_GEN)
-    tile_epilogue_wp<EK>(g, e, acc, smem, m0, n0, wr, wc, lane);
-  else
-    tile_epilogue<256, 256, 2, 4, MT, 2, 4 * STAGE, EK>(g, e, acc, smem, m0, n0, (int)blockIdx.y, wr, wc, lane);
-}
-// (NST = 5: five 32 KB stages = all 160 KB of the CU's LDS, no room for the work-queue hand-off word:
-// fixed stride only)
 
 // ---- Pipelined schedule for the plain kind (EPI_STORE, MT 16): a tile's epilogue overlaps the next
 // tile's first operand loads and its own store drain overlaps the next tile's first K-tile.
@@ -1758,27 +1522,20 @@ FER_DEV void tile_rpp(const GemmArgs& g, const EpiArgs& e, int bid, char* smem, 
 // tile on, a spilled SGPR pair reloaded by v_readlane right before the inline-asm claim atomic that
 // takes it as its address, without the 5 wait states "VALU writes SGPR -> VMEM reads it" needs (LLVM
 // does not look inside inline asm); the build pass (store_hazard_pad.py) now pads every such site.
-// The gate and row-operand kinds (FER_PP_KINDS=1, epilogue fields by value in PpEpiX) then pass the
-// kernel tests but measured slower (profiles/r05y_*: gate-mul +16 us, fc2 fwd +2-5 us, the step +0.3
-// ms), so they are built only on request (make EXTRA=-DFER_PP_KINDS=1).
-// PP_SV(EK): the vector-memory instructions every wave's epilogue issues after pro_8ph, all of them
-// unconditional (FER_OOB offsets): 16 output stores; GATE / GATER 16 pre-activation gate stores (the
-// row operand of RES / MUL is loaded before pro_8ph). Anything the compiler adds only makes the next
+// The gate and row-operand kinds on this schedule (round 5, epilogue fields by value) passed the kernel
+// tests but measured slower (profiles/r05y_*, r05ad_*: gate-mul +16 us, fc2 fwd +2-5 us, the step
+// +0.3 ms) and were removed in round 6: only the plain kind is pipelined.
+// PP_SV: the vector-memory instructions every wave's epilogue issues after pro_8ph, all of them
+// unconditional (FER_OOB offsets): its 16 output stores. Anything the compiler adds only makes the next
 // tile's first waits stricter; the epilogue's compiler barriers keep its memory operations on their
 // side of pro_8ph.
-#ifndef FER_PP_KINDS
-#define FER_PP_KINDS 0
-#endif
 template <int EK>
 constexpr int pp_sv() {
-  constexpr int S = epi_base(EK);
-  return 16 + ((S == EPI_GATE || S == EPI_GATER) ? 16 : 0);
+  return 16;
 }
-// FER_PP_KINDS bits: 1 the gate kinds (GATE, GATER), 2 RES2, 4 MUL2
 template <int EK>
 constexpr bool pp_kind() {
-  return EK == EPI_STORE || ((FER_PP_KINDS & 1) && (EK == EPI_GATE || EK == EPI_GATER)) ||
-         ((FER_PP_KINDS & 2) && EK == EPI_RES2) || ((FER_PP_KINDS & 4) && EK == EPI_MUL2);
+  return EK == EPI_STORE;
 }
 
 // Always exactly ten instructions per wave, without a branch (the epilogue's compiler-placed waits
@@ -1853,115 +1610,6 @@ FER_DEV void epi_8ph_pp(const GemmArgs& g, const PpEpi& e, f32x4 (&acc)[4][8], c
       const int row = rw0 + c * 16 + p * 8;
       const uint32_t oc = (nok && row < g.M) ? (uint32_t)row * ldcb + (uint32_t)n * 2 : FER_OOB;
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, pack8(v0, v1)), rc, oc, 0, 0);
-    }
-  }
-  bar_lds();  // the staging area is K-tile 1's B units
-}
-
-// The pipelined schedule's epilogue for the gate and row-operand kinds: the staging of epi_8ph_pp
-// (eight 16-row chunks through the wave's 4 KB of stage 1's B units) feeding the fixed-kind
-// arithmetic of tile_epilogue_wp (epi8_kb, same operations in the same order, so bit-identical to
-// the plain schedule; the MUL column sums walk each lane's rows in the same ascending order). The
-// bias and all eight chunks' row operand (64 VGPRs) are loaded before the next tile's prologue DMA.
-struct PpEpiX {
-  void* c;
-  void* pre;
-  const void* x;  // row operand: res (RES) or aux (MUL)
-  const float* bias;
-  long ldc, ldp, ldx;
-  float alpha, drop_scale;
-  uint32_t drop_thresh, drop_ld;
-  uint64_t seed;
-};
-template <bool AKC, bool BKC, int MT, int EK>
-FER_DEV void epi_8ph_ppx(const GemmArgs& g, const PpEpiX& e, f32x4 (&acc)[4][8], char* smem, int m0, int n0,
-                         int wave, int lane, int next) {
-  constexpr int UNIT = 16384, BUF = 4 * UNIT;
-  constexpr int S = epi_base(EK);
-  constexpr bool X = S == EPI_RES || S == EPI_MUL;
-  constexpr bool CS = S == EPI_MUL;
-  const int wr = wave >> 2, wc = wave & 3;
-  const int prow = lane >> 3, pc = 8 * (lane & 7);
-  const int n = n0 + wc * 64 + pc;
-  const bool nok = n < g.N;  // N % 8 == 0 on this path (checked by the host)
-  const float dsc = e.drop_thresh ? e.drop_scale : 1.f;
-  const float ab = (S == EPI_RES || EK == EPI_GATER) ? e.alpha * dsc : e.alpha;
-  const f32x2 ghs = f32x2(0.5f * dsc), gps = f32x2(0.39894228040143268f * dsc);
-  const uint64_t seed = e.drop_thresh ? step_seed(e.seed) : 0;
-  const __amdgpu_buffer_rsrc_t rbias = make_rsrc(e.bias ? (const void*)e.bias : e.c);
-  const uint32_t boff = (e.bias && nok) ? (uint32_t)n * 4 : FER_OOB;
-  f32x4 b0 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rbias, boff, 0, 0));
-  f32x4 b1 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rbias, boff + 16, 0, 0));
-  const __amdgpu_buffer_rsrc_t rc = make_rsrc(e.c), rp = make_rsrc(e.pre ? e.pre : e.c);
-  const __amdgpu_buffer_rsrc_t rx = make_rsrc(X && e.x ? e.x : e.c);
-  const uint32_t ldcb = (uint32_t)e.ldc * 2, ldpb = (uint32_t)e.ldp * 2, ldxb = X ? (uint32_t)e.ldx * 2 : 0u;
-  const int rw0 = m0 + wr * 128 + prow;  // this lane's row in pass 0 of chunk 0
-  auto load_x = [&](int c, bf16x8 (&xc)[2]) {
-#pragma unroll
-    for (int p = 0; p < 2; ++p) {
-      const int row = rw0 + c * 16 + p * 8;
-      const uint32_t off = (nok && row < g.M) ? (uint32_t)row * ldxb + (uint32_t)n * 2 : FER_OOB;
-      xc[p] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rx, off, 0, 0));
-    }
-  };
-  // every chunk's row operand before the next tile's prologue DMA: a load issued after the DMA would
-  // make the wait for it (in-order vmcnt) wait for the DMA and the earlier stores too
-  bf16x8 xr[8][2];
-  if constexpr (X) {
-#pragma unroll
-    for (int c = 0; c < 8; ++c) load_x(c, xr[c]);
-  }
-  asm volatile("" ::: "memory");
-  pro_8ph<AKC, BKC, MT, EK>(g, next, smem, wave, lane);
-  asm volatile("" ::: "memory");
-  if (S == EPI_RES || EK == EPI_GATER) {
-    b0 *= dsc;
-    b1 *= dsc;
-  }
-  f32x4 cs0 = f32x4{0.f, 0.f, 0.f, 0.f}, cs1 = cs0;
-  char* const ws = smem + BUF + 2 * UNIT + wave * 4096;
-  auto swz = [](int row, int c16) { return row * 256 + ((c16 ^ row) << 4); };
-#pragma unroll
-  for (int c = 0; c < 8; ++c) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) *(f32x4*)(ws + swz(lane & 15, 4 * i + (lane >> 4))) = acc[i][c];
-    // (a wave's own LDS accesses complete in order: no barrier)
-#pragma unroll
-    for (int p = 0; p < 2; ++p) {
-      const int lrow = p * 8 + prow;
-      f32x4 v0 = *(const f32x4*)(ws + swz(lrow, pc >> 2)), v1 = *(const f32x4*)(ws + swz(lrow, (pc >> 2) + 1));
-      const int row = rw0 + c * 16 + p * 8;
-      const bool ok = nok && row < g.M;
-      const uint32_t di = (uint32_t)row * e.drop_ld + (uint32_t)n;
-      epi8_kb<EK>(e, ok ? (uint32_t)row * ldcb + (uint32_t)n * 2 : FER_OOB,
-                  ok ? (uint32_t)row * ldpb + (uint32_t)n * 2 : FER_OOB, di, v0, v1, b0, b1,
-                  X ? xr[c][p] : bf16x8{}, seed, ab, ghs, gps, dsc, rc, rp);
-      if constexpr (CS) {
-        cs0 += ok ? v0 : f32x4{0.f, 0.f, 0.f, 0.f};
-        cs1 += ok ? v1 : f32x4{0.f, 0.f, 0.f, 0.f};
-      }
-    }
-  }
-  if constexpr (CS) {
-    if (g.cs_part) {
-      // over the 8 row lanes of the column group (lanes 8 apart), fixed order
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-#pragma unroll
-        for (int d = 8; d < 64; d <<= 1) {
-          cs0[r] += __shfl_xor(cs0[r], d);
-          cs1[r] += __shfl_xor(cs1[r], d);
-        }
-      }
-      float* red = (float*)(smem + BUF + 2 * UNIT);  // [2 wave-row halves][256 columns]
-      bar_lds();                                     // every wave is done with its staging
-      if (prow == 0) {
-        *(f32x4*)(red + wr * 256 + wc * 64 + pc) = cs0;
-        *(f32x4*)(red + wr * 256 + wc * 64 + pc + 4) = cs1;
-      }
-      bar_lds();
-      const int t = threadIdx.x;
-      if (t < 256 && n0 + t < g.N) g.cs_part[(long)(m0 / 256) * g.N + n0 + t] = red[t] + red[256 + t];
     }
   }
   bar_lds();  // the staging area is K-tile 1's B units
@@ -2103,10 +1751,7 @@ FER_DEV int tile_8ph_pp(const GemmArgs& g, const EP& e, int bid, char* smem, lds
     if (next >= g.tiles_m * g.tiles_n) next = -1;
   }
 
-  if constexpr (EK == EPI_STORE)
-    epi_8ph_pp<AKC, BKC, MT>(g, e, acc, smem, m0, n0, wave, lane, next);
-  else
-    epi_8ph_ppx<AKC, BKC, MT, EK>(g, e, acc, smem, m0, n0, wave, lane, next);
+  epi_8ph_pp<AKC, BKC, MT>(g, e, acc, smem, m0, n0, wave, lane, next);
   return next;
 }
 
@@ -2118,11 +1763,11 @@ FER_DEV int tile_8ph_pp(const GemmArgs& g, const EP& e, int bid, char* smem, lds
 // XCD tile_of's remap gives it): the first tile is blockIdx.x, each tile claims the next one at
 // its start (tile_8ph claim_slot) and hands it on through LDS at its end. !DYN: fixed stride
 // (split-K launches, stream capture, fer_set_persistent_mode).
-template <bool AKC, bool BKC, int MT, bool DYN, int EK, int HR = 128>
+template <bool AKC, bool BKC, int MT, bool DYN, int EK>
 __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmArgs g, EpiArgs e) {
   __shared__ __attribute__((aligned(1024))) char smem[8 * 16384 + 16];
   const int ntiles = g.tiles_m * g.tiles_n;
-  if constexpr (MT == 16 && HR == 128 && pp_kind<EK>()) {
+  if constexpr (MT == 16 && pp_kind<EK>()) {
     lds_vint* slot = DYN ? FER_LDS_INT(smem + 8 * 16384) : nullptr;
     int bid = DYN ? wq_first(ntiles) : ((int)blockIdx.x < ntiles ? (int)blockIdx.x : -1);
     if (bid < 0) return;
@@ -2136,16 +1781,11 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmArgs g, EpiArgs e)
 #pragma unroll 1
       while (bid >= 0) bid = tile_8ph_pp<AKC, BKC, MT, EK, true>(g, pe, bid, smem, slot);
     };
-    if constexpr (EK == EPI_STORE) {
-      run(PpEpi{e.c, e.bias, (long)e.ldc, e.alpha});
-    } else {
-      run(PpEpiX{e.c, e.pre, e.res ? e.res : e.aux, e.bias, (long)e.ldc, (long)e.ldp, (long)(e.res ? e.ldr : e.ldx),
-                 e.alpha, e.drop_scale, e.drop_thresh, (uint32_t)e.drop_ld, e.seed});
-    }
+    run(PpEpi{e.c, e.bias, (long)e.ldc, e.alpha});
   } else if constexpr (!DYN) {
 #pragma unroll 1
     for (int bid = blockIdx.x; bid < ntiles; bid += gridDim.x) {
-      tile_8ph<AKC, BKC, MT, EK, HR>(g, e, bid, smem, nullptr);
+      tile_8ph<AKC, BKC, MT, EK>(g, e, bid, smem, nullptr);
       bar_lds();  // every wave is done with the epilogue's LDS before the next tile's DMA
     }
   } else {
@@ -2153,32 +1793,7 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmArgs g, EpiArgs e)
     int bid = wq_first(ntiles), par = 0;
 #pragma unroll 1
     while (bid >= 0) {
-      tile_8ph<AKC, BKC, MT, EK, HR>(g, e, bid, smem, slot + par);
-      bar_lds();  // every wave is done with the epilogue's LDS before the next tile's DMA
-      bid = __builtin_amdgcn_readfirstlane(slot[par]);
-      par ^= 1;
-    }
-  }
-}
-
-// Persistent launch of the ring ping-pong main loop (tile_rpp), walking tiles as gemm_8ph_kernel does.
-template <bool AKC, bool BKC, bool DYN, int EK, int NST = 4>
-__global__ __launch_bounds__(512, 1) void gemm_rpp_kernel(GemmArgs g, EpiArgs e) {
-  static_assert(NST == 4 || !DYN, "the work-queue word needs LDS beyond the ring");
-  __shared__ __attribute__((aligned(1024))) char smem[NST == 4 ? 8 * 16384 + 16 : NST * 32768];
-  const int ntiles = g.tiles_m * g.tiles_n;
-  if constexpr (!DYN) {
-#pragma unroll 1
-    for (int bid = blockIdx.x; bid < ntiles; bid += gridDim.x) {
-      tile_rpp<AKC, BKC, EK, NST>(g, e, bid, smem, nullptr);
-      bar_lds();  // every wave is done with the epilogue's LDS before the next tile's DMA
-    }
-  } else {
-    lds_vint* slot = FER_LDS_INT(smem + 8 * 16384);
-    int bid = wq_first(ntiles), par = 0;
-#pragma unroll 1
-    while (bid >= 0) {
-      tile_rpp<AKC, BKC, EK>(g, e, bid, smem, slot + par);
+      tile_8ph<AKC, BKC, MT, EK>(g, e, bid, smem, slot + par);
       bar_lds();  // every wave is done with the epilogue's LDS before the next tile's DMA
       bid = __builtin_amdgcn_readfirstlane(slot[par]);
       par ^= 1;
@@ -2449,21 +2064,13 @@ static int launch_ring(GemmArgs g, const EpiArgs& e, hipStream_t st) {
   return 0;
 }
 
-static int g_row_tile = 256;  // fer_gemm_set_row_tile
-// main loop of the 256^2 persistent kernel: 0 the 8-phase loop, 1 the ring ping-pong loop (tile_rpp);
-// fer_gemm_set_main_loop, FERVIT_GEMM_LOOP at start-up
-static int g_loop = [] {
-  const char* s = getenv("FERVIT_GEMM_LOOP");
-  return s ? atoi(s) : 0;
-}();
+
 
 template <bool AKC, bool BKC, int MT>
 static int launch_8ph(GemmArgs g, const EpiArgs& e, hipStream_t st) {
   // fixed-flag epilogues for the K-contiguous MT16 kernel (the forward and transposed-shadow dgrad path)
   const int ek = (AKC && BKC && MT == 16 && !g.partial) ? epi_kind(e, g.M, g.N) : EPI_GEN;
-  // 224-row tiles (fer_gemm_set_row_tile) for the residual kind of the N <= 768 linears
-  const bool r224 = g_row_tile == 224 && ek == EPI_RES2 && g.N <= 768 && g.splits == 1;
-  g.tiles_m = r224 ? (g.M + 223) / 224 : (g.M + 255) / 256;
+  g.tiles_m = (g.M + 255) / 256;
   g.tiles_n = (g.N + 255) / 256;
   static const int ncu = [] {
     int dev = 0, n = 0;
@@ -2477,7 +2084,7 @@ static int launch_8ph(GemmArgs g, const EpiArgs& e, hipStream_t st) {
   const int gx = std::min(ntiles, std::max(8, ncu / 8 * 8));
   g.tq = nullptr;
   WqArgs w{};
-  if (!fixed_stride_mode() && g.splits == 1 && !(MT == 16 && g_loop == 2)) {  // (loop 2: fixed stride)
+  if (!fixed_stride_mode() && g.splits == 1) {
     w = wq_prepare_here(st, gx, ntiles);
     g.tq = w.q;
     for (int c = 0; c < 8; ++c) g.tq_base[c] = w.base[c];
@@ -2496,55 +2103,6 @@ static int launch_8ph(GemmArgs g, const EpiArgs& e, hipStream_t st) {
     }                                                  \
   } else {                                             \
     FER_8PH(DY, EPI_GEN);                              \
-  }
-  if (MT == 16 && g_loop == 2 && !r224) {  // five-stage ring ping-pong, fixed stride (experiment)
-    g.tq = nullptr;
-    if constexpr (AKC && BKC) {
-      switch (ek) {
-        case EPI_STORE: hipLaunchKernelGGL((gemm_rpp_kernel<AKC, BKC, false, EPI_STORE, 5>), grid, dim3(512), 0, st, g, e); break;
-        case EPI_GATE: hipLaunchKernelGGL((gemm_rpp_kernel<AKC, BKC, false, EPI_GATE, 5>), grid, dim3(512), 0, st, g, e); break;
-        case EPI_RES2: hipLaunchKernelGGL((gemm_rpp_kernel<AKC, BKC, false, EPI_RES2, 5>), grid, dim3(512), 0, st, g, e); break;
-        case EPI_MUL2: hipLaunchKernelGGL((gemm_rpp_kernel<AKC, BKC, false, EPI_MUL2, 5>), grid, dim3(512), 0, st, g, e); break;
-        default: hipLaunchKernelGGL((gemm_rpp_kernel<AKC, BKC, false, EPI_GEN, 5>), grid, dim3(512), 0, st, g, e); break;
-      }
-    } else {
-      hipLaunchKernelGGL((gemm_rpp_kernel<AKC, BKC, false, EPI_GEN, 5>), grid, dim3(512), 0, st, g, e);
-    }
-    wq_check_launch(st, w);
-    return 0;
-  }
-  if (MT == 16 && g_loop == 1 && !r224) {  // ring ping-pong main loop (fer_gemm_set_main_loop)
-#define FER_RPP(DY, K) hipLaunchKernelGGL((gemm_rpp_kernel<AKC, BKC, DY, K>), grid, dim3(512), 0, st, g, e)
-#define FER_RPP_K(DY)                                  \
-  if constexpr (AKC && BKC) {                          \
-    switch (ek) {                                      \
-      case EPI_STORE: FER_RPP(DY, EPI_STORE); break;   \
-      case EPI_GATE: FER_RPP(DY, EPI_GATE); break;     \
-      case EPI_GATER: FER_RPP(DY, EPI_GATER); break;   \
-      case EPI_RES2: FER_RPP(DY, EPI_RES2); break;     \
-      case EPI_MUL2: FER_RPP(DY, EPI_MUL2); break;     \
-      default: FER_RPP(DY, EPI_GEN); break;            \
-    }                                                  \
-  } else {                                             \
-    FER_RPP(DY, EPI_GEN);                              \
-  }
-    if (g.tq) {
-      FER_RPP_K(true)
-    } else {
-      FER_RPP_K(false)
-    }
-#undef FER_RPP_K
-#undef FER_RPP
-    wq_check_launch(st, w);
-    return 0;
-  }
-  if constexpr (AKC && BKC && MT == 16) {
-    if (r224) {
-      if (g.tq) hipLaunchKernelGGL((gemm_8ph_kernel<AKC, BKC, MT, true, EPI_RES2, 112>), grid, dim3(512), 0, st, g, e);
-      else hipLaunchKernelGGL((gemm_8ph_kernel<AKC, BKC, MT, false, EPI_RES2, 112>), grid, dim3(512), 0, st, g, e);
-      wq_check_launch(st, w);
-      return 0;
-    }
   }
   if (g.tq) {
     FER_8PH_K(true)
@@ -2607,40 +2165,6 @@ static int dispatch_tile(int cfg, GemmArgs g, const EpiArgs& e, hipStream_t st) 
       else return launch_bf16<128, 128, 2, 2, AKC, BKC, 16>(g, e, st);
     default: return launch_8ph<AKC, BKC, 16>(g, e, st);
   }
-}
-
-// Host: the tile-ticket counters of the split-K fold for launches on `st` (null: none left -- the
-// launch then reduces with splitk_reduce_kernel). One slot of fer_tick per (device, stream), as the
-// work queues: concurrent ring launches on different streams never share counters.
-// (off by default: the reading split runs alone on its CU, and reading S slabs there costs more than the
-// separate reduction launch -- fc1 / qkv / out_proj / fc2 weight gradients alone 301 / 277 / 250 / 316 us
-// folded vs 254 / 203 / 89 / 262 us with the launch, the step 36.83 vs 36.62 ms: profiles/r05r_*)
-static int g_fold = 0;  // fer_gemm_set_splitk_fold
-static unsigned* tick_slot(hipStream_t st) {
-  static std::mutex mu;
-  static std::map<std::pair<int, hipStream_t>, unsigned*> slots;
-  static std::map<int, std::pair<unsigned*, int>> pools;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-  std::lock_guard<std::mutex> lk(mu);
-  const auto key = std::make_pair(dev, st);
-  auto it = slots.find(key);
-  if (it != slots.end()) return it->second;
-  auto pit = pools.find(dev);
-  if (pit == pools.end()) {
-    unsigned* pool = nullptr;
-    if (hipGetSymbolAddress((void**)&pool, HIP_SYMBOL(fer_tick)) != hipSuccess) pool = nullptr;
-    pit = pools.emplace(dev, std::make_pair(pool, 0)).first;
-  }
-  if (!pit->second.first || pit->second.second >= FER_TICK_SLOTS) return nullptr;
-  unsigned* s = pit->second.first + FER_TICK_TILES * pit->second.second++;
-  slots.emplace(key, s);
-  return s;
-}
-// epilogues the fold implements: fp32 output (+ accumulate, alpha), nothing else
-static bool fold_epilogue(const EpiArgs& e) {
-  return e.c_f32 && !e.bias && !(e.act & 15) && !e.pre && !e.res && !e.drop_thresh && !e.aux && !e.post_scale &&
-         !e.colsum;
 }
 
 int gemm_launch(const GemmDesc& d, const EpiArgs& e_in, hipStream_t st) {
@@ -2725,13 +2249,6 @@ int gemm_launch(const GemmDesc& d, const EpiArgs& e_in, hipStream_t st) {
   if (splits > 1) g.splits = (d.K + g.k_chunk - 1) / g.k_chunk;
   g.partial = g.splits > 1;
   g.ws = d.ws;
-  if (g.partial && g_fold && cfg >= 5 && cfg <= 7 && fold_epilogue(e)) {
-    const int bt = cfg == 5 ? 256 : 128;
-    const long tiles = (long)((d.M + bt - 1) / bt) * ((d.N + bt - 1) / bt);
-    if (tiles <= FER_TICK_TILES && d.M % bt == 0 && d.N % bt == 0 && (long)g.splits * d.M * d.N * 4 < 0x7FFFFFF0L &&
-        ((long)(d.M - 1) * e.ldc + d.N) * 4 < 0x7FFFFFF0L)
-      g.tick = tick_slot(st);
-  }
   g.cs_part = e.colsum ? reduction_ws(d.ws, (size_t)((d.M + (cfg_is_256(cfg) ? 255 : 127)) / (cfg_is_256(cfg) ? 256 : 128)) * d.N * 4,
                                       d.N, st)
                        : nullptr;
@@ -2746,7 +2263,7 @@ int gemm_launch(const GemmDesc& d, const EpiArgs& e_in, hipStream_t st) {
                 nullptr, st);
     rc = hip_check("gemm_colsum_reduce");
   }
-  if (rc || !g.partial || g.tick) return rc;
+  if (rc || !g.partial) return rc;
   const long work = (long)d.M * (d.N / 4);
   const int blocks = (int)std::min<long>((work + 255) / 256, 4096);
   hipLaunchKernelGGL(splitk_reduce_kernel<bf16>, dim3(blocks), dim3(256), 0, st, d.ws, g.splits, (long)d.M,
@@ -2838,21 +2355,7 @@ extern "C" int64_t fer_gemm_colsum_ws(int M, int N) {
   return (int64_t)std::max(fer::ceil_div(std::max(M, 1), 128), 256) * N * 4;
 }
 
-extern "C" int fer_gemm_set_splitk_fold(int on) {
-  fer::g_fold = on ? 1 : 0;
-  return 0;
-}
 
-extern "C" int fer_gemm_set_main_loop(int loop) {
-  if (loop < 0 || loop > 2) return fer::set_error("gemm_set_main_loop: 0 (8-phase), 1 (ring ping-pong), 2 (its 5-stage form)");
-  fer::g_loop = loop;
-  return 0;
-}
-extern "C" int fer_gemm_set_row_tile(int rows) {
-  if (rows != 256 && rows != 224) return fer::set_error("gemm_set_row_tile: 256 or 224");
-  fer::g_row_tile = rows;
-  return 0;
-}
 
 extern "C" int fer_gemm_set_config(int cfg) {
   if (cfg < -1 || cfg > 11) return fer::set_error("gemm_set_config: cfg must be -1 (automatic) or 0..11");

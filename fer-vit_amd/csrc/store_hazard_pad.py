@@ -1,17 +1,21 @@
 """Build step: pad gfx950 device assembly so that no VALU instruction (or data-returning LDS instruction)
-overwrites a VGPR / AGPR that a preceding vector-memory store or atomic reads (its data or its address)
-within W issue slots.
+overwrites a VGPR / AGPR holding the DATA of a preceding vector-memory store or atomic within W issue
+slots (default W = 4).
 
-Why: on MI355X the hardware read of a store's operands can trail its issue by more than the wait
-states the compiler accounts for (LLVM pads a VALU write of a >8-byte store's data by 2 wait states on
-gfx940+, and the address not at all). Measured here (profiles/r05_store_war_*):
-  * a dwordx4 buffer store, two SALU instructions, then a v_pk_mul_f32 writing the store's first data
-    pair: the store wrote the new value of one dword in lanes 12-15 of every 16 (the in-launch split-K
-    fold, every launch);
-  * the 128^2 GEMM's staged epilogue: a global_store_dwordx4 whose address pair is advanced by a
-    v_lshl_add_u64 four slots later: one 8-row pass of a tile left unwritten about once in 40 launches.
+Why: on MI355X the hardware read of a store's data registers can trail its issue by more than the wait
+states the compiler accounts for. Measured (DESIGN.md sections 10-11, profiles/r05_store_war_*,
+profiles/r06a_store_pad_window.txt): the in-launch split-K fold's buffer_store_dwordx4, followed within two
+slots by VALU writes of its data registers (v_pk_mul_f32 among others), stored the new value of one dword
+in 4 lanes of 16 on every launch. One library per pass setting, each running that reproducer once
+(round 6): no pads -> wrong values; every operand (data and address) at W = 2, 4, 8 -> exact; data
+operands only at W = 2, 4, 16 -> exact; address operands only at W = 16 -> wrong; v_pk_* writers only at
+W = 16 -> wrong. So the class is "a VALU / LDS-read write of a store's DATA registers" (any opcode), and a
+2-slot window suffices on that reproducer; the default keeps twice that. (The 128^2 epilogue's
+"address-register" case of round 5 was the LDS race its barrier fixed: profiles/r05p_gemm128_stress_after_fix.txt,
+0 of 149 with no pads at all.) PAD_W / PAD_CLASS (data | addr | all) / PAD_WRITER (an opcode prefix) select
+other settings for experiment builds.
 The pass walks each store's following instructions in program order; when a VALU (v_*) or an LDS read writes one of
-the store's registers less than W slots after it, an s_nop of the missing slots goes in front of that
+the tracked registers less than W slots after it, an s_nop of the missing slots goes in front of that
 instruction, on every path: branches are followed into their targets (both successors of a conditional
 branch). Every other instruction is left as it is.
 
@@ -30,7 +34,8 @@ import os
 import re
 import sys
 
-W_DEFAULT = 16
+W_DEFAULT = 4
+CLASS_DEFAULT = "data"
 
 # vector-memory stores and atomics (an atomic reads its address and data registers the same way)
 STORE = re.compile(r"^\s*((global|buffer|flat|scratch)_store_\w+|(global|buffer|flat)_atomic_\w+)")
@@ -49,17 +54,28 @@ def regs(text):
     return out
 
 
+def data_index(op, mods):
+    """Operand position of a store's / atomic's data: buffer_* puts vdata first; global_ / flat_ / scratch_
+    stores put the address first (vaddr, vdata, ...); a returning global / flat atomic (sc0) has vdst,
+    vaddr, vdata."""
+    if op.startswith("buffer_"):
+        return 0
+    if "_atomic" in op and re.search(r"\bsc0\b", mods):
+        return 2
+    return 1
+
+
 def store_regs(line, cls="all"):
-    """Registers a store reads: every v/a register among its operands (data and address). cls (PAD_CLASS,
-    experiment builds only): "data" = only the data operand (the first one of a store, the second of an
-    atomic), "addr" = only the rest."""
-    body = line.split(None, 1)[1] if len(line.split(None, 1)) > 1 else ""
+    """Registers a store reads: every v/a register among its operands (data and address). cls: "data" =
+    only the data operand, "addr" = only the rest."""
+    parts = line.split(None, 1)
+    body = parts[1] if len(parts) > 1 else ""
     body = body.split("//")[0].split(";")[0]
     if cls == "all":
         return regs(body)
     ops = [o.strip() for o in body.split(",")]
-    di = 1 if "atomic" in line.split(None, 1)[0] else 0
-    data = regs(ops[di]) if len(ops) > di else set()
+    di = data_index(parts[0].strip(), body)
+    data = regs(ops[di].split()[0]) if len(ops) > di and ops[di] else set()
     return data if cls == "data" else regs(body) - data
 
 
@@ -107,7 +123,7 @@ def nops(n, indent="\t"):
     return out
 
 
-def pad(lines, W):
+def pad(lines, W, cls=CLASS_DEFAULT):
     """Pads in front of every VALU / LDS-read write of a store's register on any path that reaches it
     less than W slots after the store: branches are followed into their targets (both ways for a
     conditional one), so a window that leaves a block is padded only where an overwrite happens."""
@@ -147,7 +163,7 @@ def pad(lines, W):
     for i, l in enumerate(lines):
         if not STORE.match(l):
             continue
-        live = store_regs(l, os.environ.get("PAD_CLASS", "all"))
+        live = store_regs(l, cls)
         if live:
             walk(i + 1, 0, live, set())
     out = []
@@ -217,13 +233,14 @@ def main():
     W = int(sys.argv[3]) if len(sys.argv) > 3 else W_DEFAULT
     with open(src) as f:
         lines = f.readlines()
-    out, n = pad(lines, W)
+    out, n = pad(lines, W, os.environ.get("PAD_CLASS", CLASS_DEFAULT))
     na = 0
     if os.environ.get("PAD_SGPR", "1") != "0":  # (PAD_SGPR=0: A/B builds only)
         out, na = pad_asm_sgpr(out)
     with open(dst, "w") as f:
         f.writelines(out)
-    print(f"store_hazard_pad: {n} pads ({W} slots), {na} inline-asm SGPR pads in {src}", file=sys.stderr)
+    print(f"store_hazard_pad: {n} pads ({W} slots, {os.environ.get('PAD_CLASS', CLASS_DEFAULT)} operands), "
+          f"{na} inline-asm SGPR pads in {src}", file=sys.stderr)
 
 
 if __name__ == "__main__":

@@ -52,9 +52,6 @@ class ImageAug(C.Structure):
 SIGNATURES = {
     "fer_gemm": (i32, [C.POINTER(GemmDesc), C.POINTER(Epilogue), vp]),
     "fer_gemm_set_config": (i32, [i32]),
-    "fer_gemm_set_row_tile": (i32, [i32]),
-    "fer_gemm_set_main_loop": (i32, [i32]),
-    "fer_gemm_set_splitk_fold": (i32, [i32]),
     "fer_set_persistent_mode": (i32, [i32]),
     "fer_stream_create_cu_mask": (i32, [C.POINTER(C.c_uint32), i32, i32, C.POINTER(C.c_void_p)]),
     "fer_stream_destroy": (i32, [vp]),

@@ -76,20 +76,6 @@ typedef struct {
 } fer_epilogue;
 
 int fer_gemm(const fer_gemm_desc* d, const fer_epilogue* e, fer_stream_t stream);
-/* Row height of the 8-phase kernel's tiles for the residual-epilogue linears with N <= 768 (ViT-B's
- * out_proj / linear2 forward and linear1 / in_proj input gradients, `image_vit.py:101-113`): 256
- * (default) or 224 (678 instead of 591 tiles at 50,432 rows: 2.65 instead of 2.31 rounds of 256 CUs). */
-int fer_gemm_set_row_tile(int rows);
-/* Main loop of the persistent 256 x 256 GEMM (every forward / input-gradient linear of
- * `image_vit.py:101-113`): 0 (default) the 8-phase loop (BK 64, two LDS stages, 16-MFMA segments),
- * 1 the ring ping-pong loop (BK 32, four LDS stages, 32-MFMA segments). Same results to rounding of
- * the K order (both accumulate K in ascending order per accumulator: bit-identical). */
-int fer_gemm_set_main_loop(int loop);
-/* Split-K GEMMs on the BK = 32 ring kernel (the MN x MN weight gradients dW = dY^T X of ViT-B's linears,
- * `image_vit.py:101-113` backward) with an fp32-output epilogue: 1 = the K splits are summed inside the
- * launch by the last split of each tile (tile tickets), 0 (default, measured faster) = a separate
- * reduction launch. Both add the splits in split order: bit-identical results. */
-int fer_gemm_set_splitk_fold(int on);
 
 /* Grouped weight gradients: dw[n][k] (+)= sum_m dy[m][n] x[m][k] (bf16 dy [M][N] row stride ld_dy,
  * bf16 x [M][K] row stride ld_x, fp32 dw [N][K] row stride ld_dw) for up to 8 nn.Linear weights

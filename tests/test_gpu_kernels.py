@@ -697,39 +697,6 @@ def test_attention_fwd_occupancy_form_bit_exact(N, H, dh, B, p):
     assert torch.equal(d1.view(torch.int16), d2.view(torch.int16))
 
 
-@pytest.mark.parametrize("M,N,K", [(50432, 768, 768), (20000, 768, 3072), (1000, 768, 520), (4000, 512, 1024),
-                                   (333, 256, 64)])
-@pytest.mark.parametrize("p", [0.0, 0.1])
-def test_gemm_row_tile_224_bit_exact(M, N, K, p):
-    """224-row tiles (fer_gemm_set_row_tile(224): the residual kind of the N <= 768 linears) against the
-    256-row tiles: every output element sums the same K in the same order, so the residual + bias +
-    dropout epilogue output must agree bit for bit; every row (including the 16 past each wave-row
-    half, whose A rows are loaded but carry no MFMA) written exactly once (NaN-prefilled output)."""
-    from fervit._lib import lib
-
-    o = ops()
-    g = torch.Generator(device=DEV).manual_seed(M + N + K)
-    x = torch.randn(M, K, device=DEV, generator=g).to(torch.bfloat16)
-    w = (torch.randn(N, K, device=DEV, generator=g) / math.sqrt(K)).to(torch.bfloat16)
-    b = torch.randn(N, device=DEV, generator=g)
-    res = torch.randn(M, N, device=DEV, generator=g).to(torch.bfloat16)
-    outs = []
-    try:
-        for rows in (256, 224):
-            assert lib().fer_gemm_set_row_tile(rows) == 0
-            y = torch.full((M, N), float("nan"), device=DEV, dtype=torch.bfloat16)
-            o.linear_fwd(x, w, b, out=y, res=res, dropout=p, seed=1234, drop_ld=N)
-            torch.cuda.synchronize()
-            outs.append(y)
-    finally:
-        lib().fer_gemm_set_row_tile(256)
-    assert torch.isfinite(outs[1].float()).all()
-    assert torch.equal(outs[0].view(torch.int16), outs[1].view(torch.int16))
-    if p == 0.0:
-        ref = x.float() @ w.float().t() + b + res.float()
-        assert rel_err(outs[1], ref) < 1e-2
-
-
 def test_gemm_work_queue_every_tile_written():
     """Work-queue claims of the pipelined plain-kind GEMM (the next tile's claim is an inline-asm atomic
     whose result is read after the main loop): a NaN-prefilled output must come back finite and equal
@@ -753,121 +720,3 @@ def test_gemm_work_queue_every_tile_written():
         torch.cuda.synchronize()
         assert torch.isfinite(y.float()).all()
         assert rel_err(y, ref) < 1e-2
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("M,N,K,acc", [(50432, 3072, 768, False), (50432, 768, 768, True), (20000, 1000, 264, True),
-                                       (16384, 2304, 768, False)])
-def test_wgrad_splitk_fold_bit_exact(M, N, K, acc):
-    """Split-K weight gradients (MN x MN ring kernel) with the in-launch fold (fer_gemm_set_splitk_fold(1),
-    tile tickets, last split sums the slabs in split order; whole tiles only -- the 1000 x 264 case takes
-    the separate reduction either way) against the separate reduction launch:
-    bit-identical, bit-identical run to run, every element written (NaN prefill when not accumulating),
-    and within bf16-input tolerance of the fp32 product. Also two streams folding at once (separate
-    ticket slots)."""
-    from fervit._lib import lib
-
-    o = ops()
-    g = torch.Generator(device=DEV).manual_seed(M + N + K)
-    dy = torch.randn(M, N, device=DEV, generator=g).to(torch.bfloat16)
-    x = torch.randn(M, K, device=DEV, generator=g).to(torch.bfloat16)
-    c0 = torch.randn(N, K, device=DEV, generator=g) if acc else torch.full((N, K), float("nan"), device=DEV)
-    outs, slabs = [], []
-    from fervit import ops as fops
-    try:
-        for fold in (0, 1, 1):
-            lib().fer_gemm_set_splitk_fold(fold)
-            c = c0.clone()
-            o.linear_wgrad(dy, x, c, accumulate=acc)
-            torch.cuda.synchronize()
-            outs.append(c)
-            ws = [b for k, b in fops.WS.buf.items() if k[1] == 1 and k[2] == torch.cuda.current_stream().cuda_stream]
-            slabs.append(ws[0][: 8 * N * K].clone() if ws else None)
-        # two streams at once, both folding
-        s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
-        ca, cb = c0.clone(), c0.clone()
-        torch.cuda.synchronize()
-        with torch.cuda.stream(s1):
-            o.linear_wgrad(dy, x, ca, accumulate=acc)
-        with torch.cuda.stream(s2):
-            o.linear_wgrad(dy, x, cb, accumulate=acc)
-        torch.cuda.synchronize()
-    finally:
-        lib().fer_gemm_set_splitk_fold(0)
-    assert torch.isfinite(outs[1]).all()
-    bad = []
-    for name, c in zip(("fold", "fold again", "stream 1", "stream 2"), outs[1:] + [ca, cb]):
-        d = c.view(torch.int32) != outs[0].view(torch.int32)
-        if d.any():
-            idx = d.nonzero()
-            t = torch.unique((idx[:, 0] // 256) * 1000 + idx[:, 1] // 256)
-            ex = (c[d] - outs[0][d]).abs().max().item()
-            rr = torch.bincount(idx[:, 0] % 256, minlength=256).nonzero().flatten()
-            cc = torch.bincount(idx[:, 1] % 256, minlength=256).nonzero().flatten()
-            ratio = (c[d] / outs[0][d])[:6].tolist()
-            bad.append(f"{name}: {int(d.sum())} elements, tiles (row*1000+col) {t[:12].tolist()}, max |diff| {ex:.3g}, "
-                       f"rows%256 {rr[:24].tolist()} ({len(rr)}), cols%256 {cc[:24].tolist()} ({len(cc)}), "
-                       f"ratio fold/ref {[round(v, 3) for v in ratio]}")
-    if bad and slabs[0] is not None:  # were the split partials themselves stored differently?
-        for f, sl in zip((1, 1), slabs[1:]):
-            d = sl.view(torch.int32) != slabs[0].view(torch.int32)
-            bad.append(f"slab fold {f}: {int(d.sum())} words differ from the reduction run's")
-    assert not bad, "; ".join(bad)
-    ref = dy.float().t() @ x.float() + (c0 if acc else 0)
-    assert rel_err(outs[1], ref) < 1e-3
-
-
-@pytest.mark.parametrize("M,N,K", [(1100, 520, 200), (20000, 3000, 520), (25600, 768, 768), (9000, 2048, 40),
-                                   (4000, 768, 3072)])
-@pytest.mark.parametrize("p", [0.0, 0.1])
-@pytest.mark.parametrize("loop", [1, 2])
-def test_gemm_main_loop_ring_pingpong(M, N, K, p, loop):
-    """The ring ping-pong main loop of the persistent 256x256 kernel (fer_gemm_set_main_loop(1): BK 32, four
-    LDS stages, one 32-MFMA segment per wave and K-step) against the 8-phase loop (0) on the same calls: every
-    fixed epilogue kind (plain, GELU gate, residual, gate multiply with column sums), the generic epilogue with
-    an MN-contiguous B operand (dgrad), ragged M / N and K tails -- bit-identical (both accumulate each output
-    in ascending K order), every element written (NaN prefill), and within bf16 tolerance of fp32 torch."""
-    from fervit._lib import lib
-
-    o = ops()
-    g = torch.Generator(device=DEV).manual_seed(M + N + K)
-    x = torch.randn(M, K, device=DEV, generator=g).to(torch.bfloat16)
-    w = (torch.randn(N, K, device=DEV, generator=g) / math.sqrt(K)).to(torch.bfloat16)
-    b = torch.randn(N, device=DEV, generator=g)
-    res = torch.randn(M, N, device=DEV, generator=g).to(torch.bfloat16)
-    dy = torch.randn(M, K, device=DEV, generator=g).to(torch.bfloat16)
-    w2 = (torch.randn(K, N, device=DEV, generator=g) / math.sqrt(N)).to(torch.bfloat16)  # [out=K, in=N]
-    nan = lambda *s: torch.full(s, float("nan"), device=DEV, dtype=torch.bfloat16)
-
-    def run():
-        out = {}
-        out["plain"] = o.linear_fwd(x, w, b, out=nan(M, N))
-        gate = nan(M, N)
-        out["gelu"] = o.linear_fwd(x, w, b, out=nan(M, N), pre=gate, pre_gate=True, act="gelu", dropout=p, seed=5)
-        out["gate"] = gate
-        out["res"] = o.linear_fwd(x, w, b, out=nan(M, N), res=res, dropout=p, seed=6)
-        cs = torch.zeros(N, device=DEV)
-        out["mul"] = o.linear_fwd(x, w, out=nan(M, N), aux=gate, aux_act="mul", colsum=cs)
-        out["mul_cs"] = cs
-        out["dgrad"] = o.linear_dgrad(dy, w2, out=nan(M, N))
-        torch.cuda.synchronize()
-        return out
-
-    lib().fer_gemm_set_config(8)
-    try:
-        lib().fer_gemm_set_main_loop(0)
-        a = run()
-        assert lib().fer_gemm_set_main_loop(loop) == 0
-        bb = run()
-        cc = run()
-    finally:
-        lib().fer_gemm_set_main_loop(0)
-        lib().fer_gemm_set_config(-1)
-    for k in a:
-        assert torch.isfinite(bb[k].float()).all(), k
-        assert torch.equal(a[k].view(torch.int16) if a[k].dtype == torch.bfloat16 else a[k],
-                           bb[k].view(torch.int16) if bb[k].dtype == torch.bfloat16 else bb[k]), k
-        assert torch.equal(bb[k], cc[k]), k
-    ref = x.float() @ w.float().t() + b
-    assert rel_err(bb["plain"], ref) < 1e-2
-    assert rel_err(bb["dgrad"], dy.float() @ w2.float()) < 1e-2

@@ -12,9 +12,9 @@ shp = importlib.util.module_from_spec(spec)
 spec.loader.exec_module(shp)
 
 
-def run(asm, W=16):
+def run(asm, W=16, cls="all"):
     lines = [l + "\n" for l in asm.strip("\n").split("\n")]
-    out, n = shp.pad(lines, W)
+    out, n = shp.pad(lines, W, cls)
     return [l.rstrip("\n") for l in out], n
 
 
@@ -37,6 +37,24 @@ def test_data_overwrite_padded_to_window():
 """)
     assert n == 1
     assert nop_slots_before(out, "v_pk_mul_f32") == 16 - 2  # two SALU slots already there
+
+
+def test_default_tracks_data_operands_in_a_4_slot_window():
+    """The shipped setting (measured class and window: profiles/r06a_store_pad_window.txt): a store's data
+    registers 4 slots, its address registers not at all."""
+    lines = [l + "\n" for l in """
+\tbuffer_store_dwordx4 v[156:159], v195, s[8:11], s12 offen
+\ts_lshl_b32 s70, s34, 6
+\tv_pk_mul_f32 v[156:157], v[192:193], v[154:155] op_sel_hi:[0,1]
+\tglobal_store_dwordx4 v[38:39], v[0:3], off
+\tv_lshl_add_u64 v[38:39], v[38:39], 0, s[4:5]
+""".strip("\n").split("\n")]
+    assert shp.W_DEFAULT == 4 and shp.CLASS_DEFAULT == "data"
+    out, n = shp.pad(lines, shp.W_DEFAULT)
+    out = [l.rstrip("\n") for l in out]
+    assert n == 1
+    assert nop_slots_before(out, "v_pk_mul_f32") == 3
+    assert nop_slots_before(out, "v_lshl_add_u64") == 0
 
 
 def test_address_overwrite_padded():

@@ -82,23 +82,7 @@ def main():
     only = os.environ.get("GB_ONLY")
     if only:
         cases = {k: v for k, v in cases.items() if only in k}
-    # GB_ROWS=ab: every case at both row tiles of fer_gemm_set_row_tile (256, 224), interleaved;
-    # GB_FOLD=ab: split-K reduction in the launch (fer_gemm_set_splitk_fold 1) and as its own launch (0)
-    from fervit._lib import lib
-
-    if os.environ.get("GB_ROWS") == "ab":
-        rows = [("rows 256", lambda: lib().fer_gemm_set_row_tile(256)), ("rows 224", lambda: lib().fer_gemm_set_row_tile(224))]
-    elif os.environ.get("GB_LOOP") == "ab":  # main loop of the 256^2 kernel: 8-phase (0) vs ring ping-pong (1)
-        def setl(loop, fixed=0):
-            def f():
-                lib().fer_gemm_set_main_loop(loop)
-                lib().fer_set_persistent_mode(fixed)
-            return f
-        rows = [("loop 0", setl(0)), ("loop 1", setl(1)), ("loop 2 fixed", setl(2, 1)), ("loop 0 fixed", setl(0, 1))]
-    elif os.environ.get("GB_FOLD") == "ab":
-        rows = [("fold 1", lambda: lib().fer_gemm_set_splitk_fold(1)), ("fold 0", lambda: lib().fer_gemm_set_splitk_fold(0))]
-    else:
-        rows = [(None, None)]
+    rows = [(None, None)]
 
     res = {(k, rt): [] for k in cases for rt, _ in rows}
     ref = {k: [] for k in cases}
@@ -110,10 +94,6 @@ def main():
                 res[(k, rt)].append(timeit(fn))
             if tf is not None:
                 ref[k].append(timeit(tf))
-    lib().fer_gemm_set_row_tile(256)
-    lib().fer_gemm_set_splitk_fold(0)
-    lib().fer_gemm_set_main_loop(0)
-    lib().fer_set_persistent_mode(0)
     tag = cfg if cfg is not None else "auto"
     for k, (fn, fl, tf) in cases.items():
         for rt, _ in rows:

@@ -1,5 +1,5 @@
 """Run-to-run bit equality of the 8-phase GEMM: the same launch repeated must give identical bits.
-Residual kind (bias + residual, no dropout) at 256- and 224-row tiles, several shapes; prints, per
+Residual kind (bias + residual, no dropout), several shapes; prints, per
 shape and tile height, how many elements differ between repeats and between the two tile heights,
 and where (row % tile height, column % 256) the differences sit."""
 import math
@@ -60,33 +60,13 @@ def main():
         w = (torch.randn(N, K, device=dev, generator=g) / math.sqrt(K)).to(torch.bfloat16)
         b = torch.randn(N, device=dev, generator=g)
         res = torch.randn(M, N, device=dev, generator=g).to(torch.bfloat16)
-        outs = {}
-        for rows in (256, 224):
-            lib().fer_gemm_set_row_tile(rows)
-            reps = []
-            for _ in range(3):
-                y = torch.full((M, N), float("nan"), device=dev, dtype=torch.bfloat16)
-                ops.linear_fwd(x, w, b, out=y, res=res)
-                torch.cuda.synchronize()
-                reps.append(y.view(torch.int16).clone())
-            outs[rows] = reps
-            d = [(reps[0] != r).sum().item() for r in reps[1:]]
-            print(f"M {M} N {N} K {K} rows {rows}: repeats differing elements {d}", flush=True)
-        lib().fer_gemm_set_row_tile(256)
-        diff = outs[256][0] != outs[224][0]
-        nd = diff.sum().item()
-        print(f"M {M} N {N} K {K}: 256 vs 224 differing elements {nd}", flush=True)
-        if nd:
-            idx = diff.nonzero()
-            r, c = idx[:, 0], idx[:, 1]
-            print("  rows % 256:", torch.bincount(r % 256, minlength=256).nonzero().flatten()[:20].tolist())
-            print("  rows % 224:", torch.bincount(r % 224, minlength=224).nonzero().flatten()[:20].tolist())
-            print("  cols % 256:", torch.bincount(c % 256, minlength=256).nonzero().flatten()[:20].tolist())
-            print("  first rows:", r[:10].tolist(), "cols:", c[:10].tolist())
-            a = outs[256][0].view(torch.bfloat16)[diff].float()[:8].tolist()
-            bb = outs[224][0].view(torch.bfloat16)[diff].float()[:8].tolist()
-            print("  values 256:", a, "\n  values 224:", bb)
-
-
+        reps = []
+        for _ in range(3):
+            y = torch.full((M, N), float("nan"), device=dev, dtype=torch.bfloat16)
+            ops.linear_fwd(x, w, b, out=y, res=res)
+            torch.cuda.synchronize()
+            reps.append(y.view(torch.int16).clone())
+        d = [(reps[0] != r).sum().item() for r in reps[1:]]
+        print(f"M {M} N {N} K {K}: repeats differing elements {d}", flush=True)
 if __name__ == "__main__":
     main()

@@ -13,7 +13,7 @@ over rounds. Variants:
   wgoff          weight gradients on the compute stream
   adamwbw        FusedAdamW.step_in_backward (per-layer updates from the backward's gradient-ready hook)
   noadamcache    FusedAdamW uploads its segment table every step (the round-4 behaviour)
-  lib:<k>=<v>    a library selector for the variant: attnfwd (fer_attention_set_fwd_kernel), gemmcfg, rowtile, fold
+  lib:<k>=<v>    a library selector for the variant: attnfwd (fer_attention_set_fwd_kernel), gemmcfg
 <pred>: lt<N> (bit < N), ge<N> (bit >= N), m<K>lt<N> (bit % K < N), m<K>ge<N> (bit % K >= N).
 """
 import argparse
@@ -99,8 +99,6 @@ def main():
     def setup(v):
         lib().fer_attention_set_fwd_kernel(0)
         lib().fer_gemm_set_config(-1)
-        lib().fer_gemm_set_row_tile(256)
-        lib().fer_gemm_set_splitk_fold(0)
         opt.step_in_backward(False)
         opt.cache_table = True
         runtime.WGRAD.enabled = True
@@ -123,8 +121,7 @@ def main():
             opt.cache_table = False
         elif body.startswith("lib:"):  # a library run-time selector, e.g. lib:attnfwd=2
             k, val = body[4:].split("=")
-            fn = {"attnfwd": "fer_attention_set_fwd_kernel", "gemmcfg": "fer_gemm_set_config",
-                  "rowtile": "fer_gemm_set_row_tile", "fold": "fer_gemm_set_splitk_fold"}[k]
+            fn = {"attnfwd": "fer_attention_set_fwd_kernel", "gemmcfg": "fer_gemm_set_config"}[k]
             check(getattr(lib(), fn)(int(val)), fn)
         elif body.startswith("wg:"):
             runtime.WGRAD.streams[dev] = masked(body[3:])
