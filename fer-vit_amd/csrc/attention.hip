@@ -44,6 +44,9 @@ FER_DEV void load_image(char* img, const bf16* src, long ld, int N, int dh) {
 }
 
 FER_DEV bf16x8 rd_row(const char* img, int r, int c) { return *(const bf16x8*)(img + img_off(r, c)); }
+// == rd_row(img, R + (lane & 31), 2s + (lane >> 5)) for img + R * 128 passed as `img`
+FER_DEV int row_base(int lane) { return (lane & 31) * 128 + (((lane >> 5) ^ swz(lane & 31)) << 4); }
+FER_DEV bf16x8 rd_rowb(const char* img, int rb, int s) { return *(const bf16x8*)(img + (rb ^ (s << 5))); }
 
 // B/A operand of the 32x32x16 MFMA built from 8 rows (k) of an image, columns cb..cb+31:
 // lane l gets column cb + (l&31), rows R+{0..3} (elements 0..3) and R+8+{0..3} (4..7),
@@ -556,14 +559,20 @@ __global__ __launch_bounds__(64 * NB) __attribute__((amdgpu_waves_per_eu(4))) vo
   const char* Ki = lds;
   const char* Vi = lds + IMG;
   const uint32_t row = drop_row(bh, N, q);
-  const uint32_t mk_off = (mask && lane < 32) ? (uint32_t)(lane * 4) : FER_OOB;
   float m = -INFINITY, l = 0.f;
   f32x16 ot[2] = {f32x16{}, f32x16{}};
+  // K row reads through one lane offset (chunk 2s + hh = chunk hh XOR 2s: rd_rowb), re-derived per key block
+  // through an opaque copy: held as four loop-invariant offsets plus the mask-store offset, the 128-VGPR
+  // budget of this form spilled them to scratch, and each block's reload waited (vmcnt(0)) for the previous
+  // block's mask store
+  const int krb = row_base(lane);
   bf16x8 kfr[4];
 #pragma unroll
-  for (int s = 0; s < 4; ++s) kfr[s] = rd_row(Ki, lane & 31, 2 * s + hh);
+  for (int s = 0; s < 4; ++s) kfr[s] = rd_rowb(Ki, krb, s);
 #pragma unroll 1
   for (int kb = 0; kb < NB; ++kb) {
+    int kr = krb;
+    asm volatile("" : "+v"(kr));
     bf16x8 vfr[2][2];
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2)
@@ -574,7 +583,7 @@ __global__ __launch_bounds__(64 * NB) __attribute__((amdgpu_waves_per_eu(4))) vo
     for (int s = 0; s < 4; ++s) st = mfma32(kfr[s], qf[s], st);
     if (kb + 1 < NB) {
 #pragma unroll
-      for (int s = 0; s < 4; ++s) kfr[s] = rd_row(Ki, (kb + 1) * 32 + (lane & 31), 2 * s + hh);
+      for (int s = 0; s < 4; ++s) kfr[s] = rd_rowb(Ki + (kb + 1) * 4096, kr, s);
     }
     if (kb == NB - 1 && NB * 32 > N) {  // only the last key block has padding keys
 #pragma unroll
@@ -620,6 +629,9 @@ __global__ __launch_bounds__(64 * NB) __attribute__((amdgpu_waves_per_eu(4))) vo
         if (mask) word |= half ? wl_keys8<8>(0u, bal) : wl_keys8<0>(0u, bal);
       }
       if (mask) {
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        const uint32_t mk_off = ln < 32 ? (uint32_t)(ln * 4) : FER_OOB;
         __builtin_amdgcn_raw_buffer_store_b32(word, rmk, mk_off,
                                               __builtin_amdgcn_readfirstlane((int)((((long)bh * NB + kb) * NB + w) * 128)), 0);
       }
@@ -711,9 +723,6 @@ FER_DEV bf16x8 rd_trb(const char* img, const TrB& b, bool hi) {
   short4_t t2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4_t*)(img + (hi ? (b.a2 ^ 64) : b.a2)));
   return cat8(t1, t2);
 }
-// == rd_row(img, R + (lane & 31), 2s + (lane >> 5)) for img + R * 128 passed as `img`
-FER_DEV int row_base(int lane) { return (lane & 31) * 128 + (((lane >> 5) ^ swz(lane & 31)) << 4); }
-FER_DEV bf16x8 rd_rowb(const char* img, int rb, int s) { return *(const bf16x8*)(img + (rb ^ (s << 5))); }
 // == rd_tr64(img, R, lane) for img + R * 64 passed as `img`
 FER_DEV int2 tr64_base(int lane) {
   const int gg = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;

@@ -1,7 +1,7 @@
 # One GPU call: a build A/B. The in-tree library (fer-vit_amd/fervit/libfervit.so) against another
 # build in the same directory ($BASE, default libfervit_base.so): the GPU tests matching $KT on the
 # in-tree library, then interleaved GEMM microbenchmarks ($GB_ONLY cases) and short bench runs on both.
-# usage: [KT=...] [GB_ONLY=...] [BASE=lib.so] [REPS=3] [CFG=bench config] [BSTEPS=30] bash tools/lib_ab.sh <tag> [tests] [gbench] [bench]
+# usage: [KT=...] [GB_ONLY=...] [BASE=lib.so] [REPS=3] [CFG=bench config] [BSTEPS=30] bash tools/lib_ab.sh <tag> [tests] [gbench] [abench] [bench]
 set -o pipefail
 TAG=${1:-ab}; shift
 STEPS=${*:-tests gbench bench}
@@ -18,6 +18,11 @@ for s in $STEPS; do
       for rep in 1 2; do for lib in $LIBS; do
         (cd tools && FERVIT_LIB=$L/$lib GB_ONLY="${GB_ONLY:-}" timeout -k 10 300 python -u gemm_bench.py 2>&1 | grep -v amdgpu.ids) \
           | sed "s/^/[$lib] /" | tee -a gpurun_out/${TAG}_gemm_ab.txt || exit 1
+      done; done ;;
+    abench)
+      for rep in 1 2; do for lib in $LIBS; do
+        (cd tools && FERVIT_LIB=$L/$lib timeout -k 10 300 python -u attn_bench.py 2>&1 | grep -v amdgpu.ids) \
+          | sed "s/^/[$lib] /" | tee -a gpurun_out/${TAG}_attn_ab.txt || exit 1
       done; done ;;
     bench)
       for rep in $(seq ${REPS:-3}); do for lib in $LIBS; do
