@@ -273,6 +273,39 @@ __global__ __launch_bounds__(256) void tokens_fwd4_kernel(const T* __restrict__ 
   }
 }
 
+// bf16 with D % 8 == 0 (ViT-B: 256 x 197 x 768): 8 consecutive d per thread (16-byte loads and stores) and
+// 32-bit index arithmetic (the 4-wide form's 64-bit divisions per element group were most of its time); the
+// same per-element values and keep bits (two keep4 per 8 elements).
+__global__ __launch_bounds__(256) void tokens_fwd8_kernel(const bf16* __restrict__ emb, const float* __restrict__ cls,
+                                                          const float* __restrict__ pos, bf16* __restrict__ t, int B,
+                                                          int n, int D, uint32_t thr, float dscale, uint64_t seed) {
+  seed = step_seed(seed);
+  const uint32_t N = n + 1, D8 = D >> 3;
+  const uint32_t total = (uint32_t)B * N * D8;  // (host: < 2^31)
+  for (uint32_t i8 = blockIdx.x * 256u + threadIdx.x; i8 < total; i8 += gridDim.x * 256u) {
+    const uint32_t row = i8 / D8, d = (i8 - row * D8) * 8;
+    const uint32_t b = row / N, tk = row - b * N;
+    f32x4 v0, v1;
+    if (tk == 0) {
+      v0 = *(const f32x4*)(cls + d);
+      v1 = *(const f32x4*)(cls + d + 4);
+    } else {
+      const bf16x8 e = *(const bf16x8*)(emb + ((long)b * n + tk - 1) * D + d);
+      v0 = f32x4{(float)e[0], (float)e[1], (float)e[2], (float)e[3]};
+      v1 = f32x4{(float)e[4], (float)e[5], (float)e[6], (float)e[7]};
+    }
+    v0 += *(const f32x4*)(pos + (long)tk * D + d);
+    v1 += *(const f32x4*)(pos + (long)tk * D + d + 4);
+    if (thr) {
+      const uint32_t idx = row * (uint32_t)D + d;
+      drop4(seed, idx, thr, dscale, v0);
+      drop4(seed, idx + 4, thr, dscale, v1);
+    }
+    *(bf16x8*)(t + (long)row * D + d) =
+        bf16x8{(bf16)v0[0], (bf16)v0[1], (bf16)v0[2], (bf16)v0[3], (bf16)v1[0], (bf16)v1[1], (bf16)v1[2], (bf16)v1[3]};
+  }
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void tokens_fwd_kernel(const T* __restrict__ emb, const float* __restrict__ cls,
                                                          const float* __restrict__ pos, T* __restrict__ t, int B,
@@ -339,6 +372,51 @@ __global__ __launch_bounds__(256) void tokens_bwd4_kernel(const T* __restrict__ 
     if (tk > 0 && demb) store4<T>(demb + ((long)b * n + tk - 1) * D + d, g);
   }
   *(f32x4*)(part + (long)blockIdx.y * cols + j) = s;
+}
+// bf16 with D % 8 == 0 (ViT-B's token gradient, 50,432 x 768): 8 consecutive columns per thread (16-byte
+// loads and stores), four batch rows in flight per iteration, and 16 batch chunks instead of 64 (a quarter
+// of the fp32 partial slabs the reduction reads: 9.7 instead of 38.7 MB at ViT-B). Per column the batch
+// rows of a chunk are summed in ascending order, as in tokens_bwd4_kernel.
+__global__ __launch_bounds__(256) void tokens_bwd8_kernel(const bf16* __restrict__ dt, bf16* __restrict__ demb, int B,
+                                                          int n, int D, uint32_t thr, float dscale, uint64_t seed,
+                                                          float* __restrict__ part, int bchunk) {
+  seed = step_seed(seed);
+  const int N = n + 1;
+  const long cols = (long)N * D;
+  const long j = (blockIdx.x * 256L + threadIdx.x) * 8;  // (token, d), d % 8 == 0
+  if (j >= cols) return;
+  const int tk = j / D, d = j - (long)tk * D;
+  const int b0 = blockIdx.y * bchunk, b1 = min(B, b0 + bchunk);
+  f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = s0;
+  auto one = [&](int b, bf16x8 v) {
+    f32x4 g0 = f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
+    f32x4 g1 = f32x4{(float)v[4], (float)v[5], (float)v[6], (float)v[7]};
+    if (thr) {
+      const uint32_t i = (uint32_t)((long)b * cols + j);
+      const uint32_t k = keep4(seed, i, thr) | (keep4(seed, i + 4, thr) << 4);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        g0[r] = (k >> r) & 1 ? g0[r] * dscale : 0.f;
+        g1[r] = (k >> (4 + r)) & 1 ? g1[r] * dscale : 0.f;
+      }
+    }
+    s0 += g0;
+    s1 += g1;
+    if (tk > 0 && demb)
+      *(bf16x8*)(demb + ((long)b * n + tk - 1) * D + d) =
+          bf16x8{(bf16)g0[0], (bf16)g0[1], (bf16)g0[2], (bf16)g0[3], (bf16)g1[0], (bf16)g1[1], (bf16)g1[2], (bf16)g1[3]};
+  };
+  int b = b0;
+  for (; b + 4 <= b1; b += 4) {
+    bf16x8 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = *(const bf16x8*)(dt + (long)(b + u) * cols + j);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) one(b + u, v[u]);
+  }
+  for (; b < b1; ++b) one(b, *(const bf16x8*)(dt + (long)b * cols + j));
+  *(f32x4*)(part + (long)blockIdx.y * cols + j) = s0;
+  *(f32x4*)(part + (long)blockIdx.y * cols + j + 4) = s1;
 }
 __global__ void tokens_bwd_final(const float* __restrict__ part, int nchunk, int N, int D, float* dcls, float* dpos,
                                  int accumulate) {
@@ -1047,6 +1125,11 @@ extern "C" int fer_tokens_fwd(int dtype, const void* emb, const float* cls, cons
   if (total <= 0) return 0;
   if (check_drop_range(drop_thresh, total, "tokens_fwd: dropout over >= 2^32 elements")) return -1;
   hipStream_t st = (hipStream_t)stream;
+  if (dtype == FER_BF16 && D % 8 == 0 && total < (1L << 31)) {
+    hipLaunchKernelGGL(tokens_fwd8_kernel, dim3(grid_for(total / 8)), dim3(256), 0, st, (const bf16*)emb, cls, pos,
+                       (bf16*)t, B, n, D, drop_thresh, drop_scale, seed);
+    return hip_check("tokens_fwd8");
+  }
   if (D % 4 == 0) {
     if (dtype == FER_BF16)
       hipLaunchKernelGGL(tokens_fwd4_kernel<bf16>, dim3(grid_for(total / 4)), dim3(256), 0, st, (const bf16*)emb, cls,
@@ -1076,8 +1159,18 @@ extern "C" int fer_tokens_bwd(int dtype, const void* dt, void* demb, float* dcls
   const int nch = tokens_chunks(B);
   if (!ws || ws_bytes < fer_tokens_bwd_ws(B, N, D)) return set_error("tokens_bwd: workspace too small");
   if (check_drop_range(drop_thresh, (long)B * N * D, "tokens_bwd: dropout over >= 2^32 elements")) return -1;
-  const int bchunk = ceil_div(B, nch);
+  int bchunk = ceil_div(B, nch);
   hipStream_t st = (hipStream_t)stream;
+  if (dtype == FER_BF16 && D % 8 == 0) {
+    const int nch8 = std::min(nch, 16);  // (the workspace is sized for tokens_chunks(B) >= nch8 slabs)
+    bchunk = ceil_div(B, nch8);
+    dim3 grid8(ceil_div((long)N * D / 8, 256), nch8);
+    hipLaunchKernelGGL(tokens_bwd8_kernel, grid8, dim3(256), 0, st, (const bf16*)dt, (bf16*)demb, B, n, D, drop_thresh,
+                       drop_scale, seed, ws, bchunk);
+    if (dpos) part_reduce(ws, nch8, (long)N * D, N * D, N * D, dpos, nullptr, nullptr, accumulate, nullptr, st);
+    if (dcls) part_reduce(ws, nch8, (long)N * D, D, D, dcls, nullptr, nullptr, accumulate, nullptr, st);
+    return hip_check("tokens_bwd8");
+  }
   if (D % 4 == 0) {
     dim3 grid4(ceil_div((long)N * D / 4, 256), nch);
     if (dtype == FER_BF16)

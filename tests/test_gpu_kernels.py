@@ -545,13 +545,14 @@ def test_colsum_and_tokens_and_head():
 
 
 @pytest.mark.parametrize("dtype", ["bf16", "fp32"])
-@pytest.mark.parametrize("D", [384, 6])
-def test_tokens_bwd_dropout(dtype, D):
+@pytest.mark.parametrize("D,B", [(384, 5), (6, 5), (388, 5), (768, 41)])
+def test_tokens_bwd_dropout(dtype, D, B):
     """Gradient of the token assembly (cat(cls, patches) + pos, dropout): d(patches), d(cls) and
-    d(pos) against the host keep mask; D % 4 == 0 takes the 4-column kernel, D = 6 the per-element
-    one (csrc/misc.hip tokens_bwd4_kernel / tokens_bwd_kernel)."""
+    d(pos) against the host keep mask; bf16 with D % 8 == 0 takes the 8-column kernel (B = 41: 16 batch
+    chunks of 3, the last ones short or empty), other D % 4 == 0 the 4-column one, D = 6 the per-element
+    one (csrc/misc.hip tokens_bwd8_kernel / tokens_bwd4_kernel / tokens_bwd_kernel)."""
     o = ops()
-    B, n, p, seed = 5, 9, 0.1, 777
+    n, p, seed = 9, 0.1, 777
     N = n + 1
     g = torch.Generator().manual_seed(21)
     cast = bf if dtype == "bf16" else (lambda t: t.to(DEV))
@@ -720,3 +721,23 @@ def test_gemm_work_queue_every_tile_written():
         torch.cuda.synchronize()
         assert torch.isfinite(y.float()).all()
         assert rel_err(y, ref) < 1e-2
+
+
+@pytest.mark.parametrize("D", [768, 388])
+def test_tokens_fwd_bf16_dropout(D):
+    """Token assembly t = dropout(cat(cls, patches) + pos) on the bf16 path: D % 8 == 0 takes the 8-column
+    kernel (csrc/misc.hip tokens_fwd8_kernel), D = 388 the 4-column one; values and keep bits against the
+    host keep mask (the same element index row * D + d in both kernels)."""
+    o = ops()
+    B, n, p, seed = 6, 13, 0.1, 4242
+    N = n + 1
+    g = torch.Generator().manual_seed(D)
+    emb = torch.randn(B * n, D, generator=g)
+    cls, pos = torch.randn(1, 1, D, generator=g), torch.randn(1, N, D, generator=g)
+    t = o.tokens_fwd(bf(emb), cls.to(DEV), pos.to(DEV), B, n, D, dropout=p, seed=seed)
+    ref = torch.cat([cls.expand(B, -1, -1), bf(emb).float().cpu().view(B, n, D)], 1) + pos
+    keep = keep_mask(seed, (B * N, D), p).view(B, N, D)
+    want = torch.where(keep, ref / (1 - p), torch.zeros(()))
+    got = t.float().cpu().view(B, N, D)
+    assert torch.equal(got != 0, keep)
+    assert rel_err(got, want) < 1e-2
