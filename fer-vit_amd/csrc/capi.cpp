@@ -25,7 +25,10 @@ int hip_check(const char* what) {
   return 0;
 }
 
-static int g_fixed_stride = 0;  // fer_set_persistent_mode
+static int g_fixed_stride = [] {  // fer_set_persistent_mode; FERVIT_FIXED_STRIDE=1 at start-up (fervit.h)
+  const char* v = getenv("FERVIT_FIXED_STRIDE");
+  return v && v[0] == '1' ? 1 : 0;
+}();
 
 bool fixed_stride_mode() { return g_fixed_stride == 1; }
 
