@@ -14,6 +14,7 @@ over rounds. Variants:
   adamwbw        FusedAdamW.step_in_backward (per-layer updates from the backward's gradient-ready hook)
   noadamcache    FusedAdamW uploads its segment table every step (the round-4 behaviour)
   lib:<k>=<v>    a library selector for the variant: attnfwd (fer_attention_set_fwd_kernel), gemmcfg
+  env:<N>=<v>    environment variable N set to v for the variant (for switches the library reads per call)
 <pred>: lt<N> (bit < N), ge<N> (bit >= N), m<K>lt<N> (bit % K < N), m<K>ge<N> (bit % K >= N).
 """
 import argparse
@@ -107,7 +108,15 @@ def main():
         runtime.WGRAD.streams[dev] = default_side["side"]
         if runtime.WGRAD.streams[dev] is None:
             del runtime.WGRAD.streams[dev]
+        for k in [k for k in os.environ if k.startswith("FERVIT_AB_")]:
+            del os.environ[k[len("FERVIT_AB_"):]]
+            del os.environ[k]
         if v == "base":
+            return None
+        if v.startswith("env:"):  # env:NAME=VALUE, read by the library at each call (on the null stream, as base)
+            name, val = v[4:].split("=", 1)
+            os.environ[name] = val
+            os.environ["FERVIT_AB_" + name] = "1"  # (undone by the next setup)
             return None
         cs = nb_compute
         body = v[3:] if v.startswith("nb:") else v
