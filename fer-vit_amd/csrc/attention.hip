@@ -253,6 +253,20 @@ FER_DEV uint32_t wl_keys8(uint32_t w, const uint64_t* b) {
   return w;
 }
 
+// wl_keys8<0> for accumulator registers 0-3 only (keys 0-7 of the block; lanes 8-31 of w unchanged)
+FER_DEV uint32_t wl_keys4(uint32_t w, const uint64_t* b) {
+  asm volatile(
+      "s_nop 4\n\t"
+      "v_writelane_b32 %0, %1, 0\n\tv_writelane_b32 %0, %2, 4\n\t"
+      "v_writelane_b32 %0, %3, 1\n\tv_writelane_b32 %0, %4, 5\n\t"
+      "v_writelane_b32 %0, %5, 2\n\tv_writelane_b32 %0, %6, 6\n\t"
+      "v_writelane_b32 %0, %7, 3\n\tv_writelane_b32 %0, %8, 7"
+      : "+v"(w)
+      : "s"((uint32_t)b[0]), "s"((uint32_t)(b[0] >> 32)), "s"((uint32_t)b[1]), "s"((uint32_t)(b[1] >> 32)),
+        "s"((uint32_t)b[2]), "s"((uint32_t)(b[2] >> 32)), "s"((uint32_t)b[3]), "s"((uint32_t)(b[3] >> 32)));
+  return w;
+}
+
 template <int NB>
 FER_DEV void fwd_dma_unit(char* buf, const u32x4& rs, int unit, long ldq, int N, int H, int dh, int lane) {
   const int b = unit / H, h = unit - b * H, D = H * dh;
@@ -569,31 +583,38 @@ __global__ __launch_bounds__(64 * NB) __attribute__((amdgpu_waves_per_eu(4))) vo
   bf16x8 kfr[4];
 #pragma unroll
   for (int s = 0; s < 4; ++s) kfr[s] = rd_rowb(Ki, krb, s);
-#pragma unroll 1
-  for (int kb = 0; kb < NB; ++kb) {
+  // key block kb; TAIL: the last block with at most 8 real keys (TAIL4 below), where only accumulator
+  // registers 0-3 (keys 0-7 of the block) can hold one: the softmax, hashing and keep-bit packing of
+  // registers 4-15 are skipped (their P is 0, as the full form computes it from -inf scores). Same
+  // results bit for bit, except the stored keep bits of padding keys: 0 here (no backward reads them).
+  auto kblock = [&](int kb, auto tail) {
+    constexpr bool TAIL = decltype(tail)::value;
+    constexpr int NR = TAIL ? 4 : 16;  // live accumulator registers
     int kr = krb;
     asm volatile("" : "+v"(kr));
+    // the tail's V offsets from a re-derived lane: from `lane` they were hoisted and spilled
+    const int lv = TAIL ? (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) : lane;
     bf16x8 vfr[2][2];
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
-      for (int db = 0; db < 2; ++db) vfr[s2][db] = rd_tr(Vi, kb * 32 + 16 * s2, db * 32, lane);
+      for (int db = 0; db < 2; ++db) vfr[s2][db] = rd_tr(Vi, kb * 32 + 16 * s2, db * 32, lv);
     f32x16 st = {};
 #pragma unroll
     for (int s = 0; s < 4; ++s) st = mfma32(kfr[s], qf[s], st);
-    if (kb + 1 < NB) {
+    if (!TAIL && kb + 1 < NB) {
 #pragma unroll
       for (int s = 0; s < 4; ++s) kfr[s] = rd_rowb(Ki + (kb + 1) * 4096, kr, s);
     }
-    if (kb == NB - 1 && NB * 32 > N) {  // only the last key block has padding keys
+    if (TAIL || (kb == NB - 1 && NB * 32 > N)) {  // only the last key block has padding keys
 #pragma unroll
-      for (int r = 0; r < 16; ++r)
+      for (int r = 0; r < NR; ++r)
         if (kb * 32 + acc_row(r, hh) >= N) st[r] = -INFINITY;
     }
     float bm = fmaxf(fmaxf(st[0], st[1]), st[2]);
 #pragma unroll
-    for (int r = 3; r < 15; r += 2) bm = fmaxf(fmaxf(bm, st[r]), st[r + 1]);
-    bm = fmaxf(bm, st[15]);
+    for (int r = 3; r < NR - 1; r += 2) bm = fmaxf(fmaxf(bm, st[r]), st[r + 1]);
+    bm = fmaxf(bm, st[NR - 1]);
     bm = xhalf_max(bm) * sl2;
     if (__builtin_amdgcn_ballot_w64(bm > m + 8.f)) {  // lazy rescale (wave-uniform), as attn_fwd_pers
       const float mn = fmaxf(m, bm);
@@ -604,21 +625,30 @@ __global__ __launch_bounds__(64 * NB) __attribute__((amdgpu_waves_per_eu(4))) vo
       ot[1] *= al;
     }
 #pragma unroll
-    for (int r = 0; r < 16; ++r) st[r] = ex2(fmaf(st[r], sl2, -m));
-    float ls[4];
+    for (int r = 0; r < 16; ++r) st[r] = r < NR ? ex2(fmaf(st[r], sl2, -m)) : 0.f;
+    if (TAIL) {
+      l += (st[0] + st[1]) + (st[2] + st[3]);  // = the tree below with registers 4-15 at 0, bit for bit
+    } else {
+      float ls[4];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) ls[c] = (st[c] + st[c + 4]) + (st[c + 8] + st[c + 12]);
-    l += (ls[0] + ls[1]) + (ls[2] + ls[3]);
+      for (int c = 0; c < 4; ++c) ls[c] = (st[c] + st[c + 4]) + (st[c + 8] + st[c + 12]);
+      l += (ls[0] + ls[1]) + (ls[2] + ls[3]);
+    }
     if (thr) {
-      const uint32_t p0 = (row >> 1) + kb * 16 + 2 * hh;
+      const uint32_t rw = TAIL ? drop_row(bh, N, w * 32 + (lv & 31)) : row;  // (re-derived: as lv)
+      const uint32_t p0 = (rw >> 1) + kb * 16 + 2 * hh;
       // two rounds of 8 ballots (16 SGPRs live instead of 32: the 16-ballot form spilled at 128 VGPRs)
       uint32_t word = 0u;
 #pragma unroll
-      for (int half = 0; half < 2; ++half) {
+      for (int half = 0; half < (TAIL ? 1 : 2); ++half) {
         uint64_t bal[8];
 #pragma unroll
         for (int r = 0; r < 8; r += 2) {
           const int rr = 8 * half + r;
+          if (rr >= NR) {
+            bal[r] = bal[r + 1] = 0;
+            continue;
+          }
           const uint32_t hv = fer_hash(seed, p0 + (uint32_t)(acc_row(rr, 0) >> 1));
           const bool k0 = (hv & 0xFFFFu) >= thr, k1 = (hv >> 16) >= thr;
           st[rr] = k0 ? st[rr] : 0.f;
@@ -626,11 +656,10 @@ __global__ __launch_bounds__(64 * NB) __attribute__((amdgpu_waves_per_eu(4))) vo
           bal[r] = __builtin_amdgcn_ballot_w64(k0);
           bal[r + 1] = __builtin_amdgcn_ballot_w64(k1);
         }
-        if (mask) word |= half ? wl_keys8<8>(0u, bal) : wl_keys8<0>(0u, bal);
+        if (mask) word |= TAIL ? wl_keys4(0u, bal) : half ? wl_keys8<8>(0u, bal) : wl_keys8<0>(0u, bal);
       }
       if (mask) {
-        int ln = lane;
-        asm volatile("" : "+v"(ln));
+        const int ln = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));  // lane, re-derived
         const uint32_t mk_off = ln < 32 ? (uint32_t)(ln * 4) : FER_OOB;
         __builtin_amdgcn_raw_buffer_store_b32(word, rmk, mk_off,
                                               __builtin_amdgcn_readfirstlane((int)((((long)bh * NB + kb) * NB + w) * 128)), 0);
@@ -642,6 +671,14 @@ __global__ __launch_bounds__(64 * NB) __attribute__((amdgpu_waves_per_eu(4))) vo
 #pragma unroll
       for (int db = 0; db < 2; ++db) ot[db] = mfma32(vfr[s2][db], pf, ot[db]);
     }
+  };
+  const bool tail4 = NB * 32 - N >= 24;  // (ViT-B/16: N = 197, 5 keys in block 6)
+#pragma unroll 1
+  for (int kb = 0; kb < NB - (tail4 ? 1 : 0); ++kb) kblock(kb, std::false_type{});
+  if (tail4) {
+    int kbt = NB - 1;  // opaque: a constant block index let the compiler hoist the tail's LDS offsets
+    asm volatile("" : "+s"(kbt));  // into the prologue, and they spilled across the loop
+    kblock(kbt, std::true_type{});
   }
   l = xhalf_sum(l);
   const float mul = dscale / l;
@@ -1821,9 +1858,11 @@ extern "C" int64_t fer_attention_ws(int dtype, int B, int N, int H) {
 
 static bool pers_path(int dtype, int N, int dh) { return dtype == FER_BF16 && N <= 224 && dh <= 64; }
 // forward kernel for N <= 224, dh <= 64 (fer_attention_set_fwd_kernel): 0 automatic (the occupancy form
-// from 4 query blocks up -- ViT-B/16's N = 197: 36.57 vs 36.87 ms per step on one box, profiles/r05d_* --
-// the persistent kernel below, where its occupancy-sized grids were tuned for the w+ / 48 px token
-// counts), 1 persistent, 2 occupancy form
+// from 4 query blocks up with dropout on -- ViT-B/16's N = 197: 36.57 vs 36.87 ms per step on one box,
+// profiles/r05d_*; alone 116 vs 125-139 us at p = 0.1 -- the persistent kernel without dropout (82 vs
+// 90 us at p = 0, profiles/r06e_attn_fwd_spill_ab.txt: its producer wave hides the K / V loads and no
+// hashing VALU is left for the occupancy form's extra waves to hide) and below 4 query blocks, where
+// its occupancy-sized grids were tuned for the w+ / 48 px token counts), 1 persistent, 2 occupancy form
 static int g_fwd_kernel = 0;
 static int64_t lse_floats(int B, int N, int H) { return ((int64_t)B * H * N + 63) / 64 * 64; }
 // persistent kernels walk a fixed blockIdx stride instead of the work queue (fer_set_persistent_mode)
@@ -1885,7 +1924,7 @@ extern "C" int fer_attention_fwd(int dtype, const void* qkv, int64_t ld_qkv, voi
     FER_NB_SWITCH(nb, hipLaunchKernelGGL(attn_fwd_bf16<NB_>, dim3(B * H), dim3(64 * NB_), 0, st, (const bf16*)qkv,
                                          (long)ld_qkv, (bf16*)out, (long)ld_out, lse, N, H, dh, sl2, drop_thresh,
                                          drop_scale, seed));
-  } else if (N <= 224 && dh <= 64 && (g_fwd_kernel == 2 || (g_fwd_kernel == 0 && (N + 31) / 32 >= 4))) {
+  } else if (N <= 224 && dh <= 64 && (g_fwd_kernel == 2 || (g_fwd_kernel == 0 && drop_thresh && (N + 31) / 32 >= 4))) {
     const int nb = (N + 31) / 32;
     uint32_t* mask = (drop_thresh && pers_path(dtype, N, dh)) ? (uint32_t*)(lse + lse_floats(B, N, H)) : nullptr;
 #define FER_FOCC2(NBV)                                                                                     \

@@ -147,12 +147,12 @@ int fer_layernorm_bwd(int dtype, const void* dy, int64_t lddy, const void* x, in
  * `saved` (saved_floats fp32 words, >= fer_attention_saved_floats(...)) is the state kept for the
  * backward: lse [B*H*N] (natural log), padded to a multiple of 64 words, then -- bf16 with dropout,
  * N <= 224, dh <= 64 -- the probability-dropout keep bits, [B*H][NB][NB][32] uint32 (NB = ceil(N/32);
- * word (kb, qb, j) = bits over the 32 queries of block qb for key kb*32 + j), so the backward does
- * not re-hash them. bf16: any N, dh <= 128, dh % 8 == 0 (persistent workgroup per CU walking the
+ * word (kb, qb, j) = bits over the 32 queries of block qb for key kb*32 + j; words of padding keys
+ * kb*32 + j >= N unspecified), so the backward does not re-hash them. bf16: any N, dh <= 128, dh % 8 == 0 (persistent workgroup per CU walking the
  * (batch, head) units for N <= 256 and dh <= 64, 128-row chunks streamed through LDS otherwise). */
 int64_t fer_attention_ws(int dtype, int B, int N, int H);
-/* Forward kernel for bf16, N <= 224, dh <= 64: 0 automatic (the occupancy form for N > 96, else the
- * persistent kernel), 1 the persistent producer / consumer kernel, 2 the occupancy form (one workgroup
+/* Forward kernel for bf16, N <= 224, dh <= 64: 0 automatic (the occupancy form for N > 96 with
+ * dropout on, else the persistent kernel), 1 the persistent producer / consumer kernel, 2 the occupancy form (one workgroup
  * per (batch, head), two per CU). Same results bit for bit. */
 int fer_attention_set_fwd_kernel(int k);
 int64_t fer_attention_saved_floats(int dtype, int B, int N, int H, int dh, uint32_t drop_thresh);

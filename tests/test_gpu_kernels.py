@@ -692,9 +692,14 @@ def test_attention_fwd_occupancy_form_bit_exact(N, H, dh, B, p):
     if p > 0:  # keep-bit words (the padding words after lse are never written by either kernel)
         nb = (N + 31) // 32
         off = (B * H * N + 63) // 64 * 64 - B * H * N
-        w1 = m1[off:off + B * H * nb * nb * 32].view(torch.int32)
-        w2 = m2[off:off + B * H * nb * nb * 32].view(torch.int32)
-        assert torch.equal(w1, w2)
+        w1 = m1[off:off + B * H * nb * nb * 32].view(torch.int32).view(B * H, nb, nb, 32)
+        w2 = m2[off:off + B * H * nb * nb * 32].view(torch.int32).view(B * H, nb, nb, 32)
+        # words of padding keys (kb*32 + j >= N) are unspecified: the occupancy form skips their hashing
+        # when the last key block holds <= 8 keys; the backward reads them but its results cannot depend
+        # on them (the dqkv comparison below)
+        real = (torch.arange(nb, device=DEV)[:, None] * 32 + torch.arange(32, device=DEV)[None, :]) < N
+        real = real[None, :, None, :].expand_as(w1)
+        assert torch.equal(w1[real], w2[real])
     assert torch.equal(d1.view(torch.int16), d2.view(torch.int16))
 
 
