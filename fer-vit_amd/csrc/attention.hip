@@ -766,6 +766,14 @@ FER_DEV int2 tr64_base(int lane) {
   const int R = 4 * (gg >> 1), c8 = 4 * (gg & 1) + p;
   return int2{ds_off(R + q, c8), ds_off(R + 8 + q, c8)};
 }
+// attn_bwd_pers' per-lane offset table entry: {row_base | tr_base.a1 << 16, tr_base.a2 | dS-write base
+// ds_off(lane & 31, lane >> 5) << 16, tr64_base.x | .y << 16, 0} (every offset < 4096)
+FER_DEV u32x4 lane_table(int lane) {
+  const TrB b = tr_base(lane);
+  const int2 t = tr64_base(lane);
+  return u32x4{(uint32_t)row_base(lane) | ((uint32_t)b.a1 << 16), (uint32_t)b.a2 | ((uint32_t)ds_off(lane & 31, lane >> 5) << 16),
+               (uint32_t)t.x | ((uint32_t)t.y << 16), 0u};
+}
 FER_DEV bf16x8 rd_tr64b(const char* img, int2 b) {
   short4_t t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4_t*)(img + b.x));
   short4_t t2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4_t*)(img + b.y));
@@ -1026,8 +1034,11 @@ __global__ __launch_bounds__(64 * NB) void attn_bwd_pers(
     int BH, int N, int H, int dh, float scale, float sl2, float dscale, float* __restrict__ cs_part, WqArgs wq) {
   constexpr int IMG = NB * 32 * 128;
   constexpr int PREP = NB >= 4 ? 3 : NB - 1;  // step whose dQ phase computes the next unit's Dq
-  __shared__ __attribute__((aligned(1024))) char lds[pers_bwd_lds_bytes<NB>() + 16];
+  __shared__ __attribute__((aligned(1024))) char lds[pers_bwd_lds_bytes<NB>() + 16 + 1024];
   lds_vint* hand = FER_LDS_INT(lds + pers_bwd_lds_bytes<NB>());  // unit hand-off (work queue)
+  // per-lane LDS offsets of the step's fragment reads and dS writes, 16-bit packed (lane_table):
+  // one ds_read_b128 per step phase instead of ~40 VALU re-deriving them from the lane id
+  const char* ltab = lds + pers_bwd_lds_bytes<NB>() + 16;
   char* Kimg = lds + 4 * IMG;               // NB x [32 keys][64 d] images
   char* Sall = lds + 5 * IMG;               // NB x [32 keys][32 queries] bf16 dS tiles
   float* lsd = (float*)(Sall + NB * 2048);  // 2 x {L[NB*32] = -lse/scale, Dq[NB*32]}
@@ -1125,6 +1136,7 @@ __global__ __launch_bounds__(64 * NB) void attn_bwd_pers(
   mwn = mask ? mwn : 0xFFFFFFFFu;
   asm volatile("" : "+v"(mwn));  // resolved after the wait: the first step's use waits for nothing
   if (wq.q && threadIdx.x == 0) hand[2] = c0;
+  if (w == 0) *(u32x4*)(lds + pers_bwd_lds_bytes<NB>() + 16 + lane * 16) = lane_table(lane);
   bar_lds();
   if (wq.q) un = __builtin_amdgcn_readfirstlane(hand[2]);
 
@@ -1173,8 +1185,9 @@ __global__ __launch_bounds__(64 * NB) void attn_bwd_pers(
         if (i == 0 && has_next) prep_issue(un, cur ^ 1);
         int qb = w + i;
         if (qb >= NB) qb -= NB;
-        const TrB tb = tr_base(lane);
-        const int rb = row_base(lane);
+        const u32x4 lt = *(const u32x4*)(ltab + lane * 16);
+        const TrB tb{(int)(lt[0] >> 16), (int)(lt[1] & 0xFFFFu)};
+        const int rb = (int)(lt[0] & 0xFFFFu), dsb = (int)(lt[1] >> 16);
         const char* Qq = Qi + qb * 4096;
         const char* Oq = Oi + qb * 4096;
         f32x16 st, dp = {};
@@ -1226,8 +1239,8 @@ __global__ __launch_bounds__(64 * NB) void attn_bwd_pers(
         }
         char* Si = Sall + w * 2048;
 #pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4)
-          *(bf16x4*)(Si + ds_off(lane & 31, 2 * g4 + hh)) =
+        for (int g4 = 0; g4 < 4; ++g4)  // ds_off(lane & 31, 2 * g4 + hh) = dsb ^ (g4 << 4)
+          *(bf16x4*)(Si + (dsb ^ (g4 << 4))) =
               bf16x4{(bf16)st[4 * g4], (bf16)st[4 * g4 + 1], (bf16)st[4 * g4 + 2], (bf16)st[4 * g4 + 3]};
         bf16x8 ot_[2][2], qt_[2][2];
 #pragma unroll
@@ -1262,8 +1275,9 @@ __global__ __launch_bounds__(64 * NB) void attn_bwd_pers(
         if (src < 0) src += NB;
         const char* So = Sall + src * 2048;
         const char* Ko = Kimg + src * 4096;
-        const TrB tb = tr_base(lane);
-        const int2 t64 = tr64_base(lane);
+        const u32x4 lt = *(const u32x4*)(ltab + lane * 16);
+        const TrB tb{(int)(lt[0] >> 16), (int)(lt[1] & 0xFFFFu)};
+        const int2 t64{(int)(lt[2] & 0xFFFFu), (int)(lt[2] >> 16)};
         bf16x8 sf[2], kt[2][2];
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {

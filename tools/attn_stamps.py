@@ -21,6 +21,7 @@ def main():
     g = torch.Generator(device="cuda").manual_seed(0)
     qkv = torch.randn(B * N, 3 * D, device="cuda", generator=g).to(torch.bfloat16)
     out = torch.empty(B * N, D, device="cuda", dtype=torch.bfloat16)
+    lib().fer_attention_set_fwd_kernel(1)  # the stamped persistent forward (the automatic choice at p > 0 is the occupancy form)
     for p in (0.1, 0.0):
         lse = ops.attention_saved(qkv, B, N, H, dh, dropout=p)
         for _ in range(3):
@@ -41,6 +42,7 @@ def main():
                 txt = " ".join(f"{n}={row[i] - base:6d}" for n, i in pts if row[i])
                 print(f"  unit{u} w{w} start={row[0] - base:6d} {txt}")
         wg_stats()
+    lib().fer_attention_set_fwd_kernel(0)
 
 
 def wg_stats():
