@@ -1041,7 +1041,7 @@ __global__ __launch_bounds__(64 * NB) void attn_bwd_pers(
   const char* ltab = lds + pers_bwd_lds_bytes<NB>() + 16;
   char* Kimg = lds + 4 * IMG;               // NB x [32 keys][64 d] images
   char* Sall = lds + 5 * IMG;               // NB x [32 keys][32 queries] bf16 dS tiles
-  float* lsd = (float*)(Sall + NB * 2048);  // 2 x {L[NB*32] = -lse/scale, Dq[NB*32]}
+  float* lsd = (float*)(Sall + NB * 2048);  // 2 x {L[NB*32] = -lse/scale, -Dq[NB*32]}
   float* csl = lsd + 4 * NB * 32;           // NB x 32: sum_q dS[q][k] of each wave's keys
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), hh = lane >> 5;
   const int D = H * dh;
@@ -1071,11 +1071,12 @@ __global__ __launch_bounds__(64 * NB) void attn_bwd_pers(
     for (int c = 0; c < 4; ++c) {
       const bf16x8 o = rd_row(Qi, r, 4 * half + c), g = rd_row(Qi + IMG, r, 4 * half + c);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) a = fmaf((float)o[e], (float)g[e], a);
+      for (int e = 0; e < 8; e += 2)  // v_dot2c_f32_bf16: one instruction per element pair (no unpacking)
+        a = __builtin_amdgcn_fdot2_f32_bf16(bf16x2{o[e], o[e + 1]}, bf16x2{g[e], g[e + 1]}, a, false);
     }
     a += __shfl_xor(a, 1, 64);
     if (!half) {
-      L[NB * 32 + r] = a;
+      L[NB * 32 + r] = -a;  // -Dq: the step's dS = P o (dP' - Dq) adds it as is
       L[r] = r < N ? -L[r] * inv_scale : -INFINITY;
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // O rows read: Q may land on them
@@ -1233,7 +1234,7 @@ __global__ __launch_bounds__(64 * NB) void attn_bwd_pers(
             // bit-identical to kp ? x : 0.f without a compare and two selects per element
             const uint32_t km = (uint32_t)((int32_t)(mws << (31 - acc_row(r, 0))) >> 31);
             pd[r] = __uint_as_float(__float_as_uint(p) & km);
-            st[r] = p * fmaf(__uint_as_float(__float_as_uint(dp[r]) & km), dscale, -d4[j]);  // dS
+            st[r] = p * fmaf(__uint_as_float(__float_as_uint(dp[r]) & km), dscale, d4[j]);  // dS (d4 = -Dq)
             cs += st[r];
           }
         }
