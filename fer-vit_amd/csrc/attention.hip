@@ -1184,6 +1184,10 @@ __global__ __launch_bounds__(64 * NB) void attn_bwd_pers(
         // unit (and its exec-masked claim atomic) and waited vmcnt(0) for all of them (~4k cycles/unit)
         asm volatile("" : "+v"(mws)::"memory");
         if (i == 0 && has_next) prep_issue(un, cur ^ 1);
+        // the next step's keep word, a whole step ahead of its use (issued in the dQ phase, its latency
+        // was exposed at the next step's start: ~500 cycles per step); after this step's DMA, so the
+        // next step's wait covers nothing issued later
+        if (i + 1 < NB) mwn = mask_word(u, i + 1);
         int qb = w + i;
         if (qb >= NB) qb -= NB;
         const u32x4 lt = *(const u32x4*)(ltab + lane * 16);
@@ -1291,7 +1295,6 @@ __global__ __launch_bounds__(64 * NB) void attn_bwd_pers(
 #pragma unroll
           for (int db = 0; db < 2; ++db) dq[db] = mfma32(kt[s2][db], sf[s2], dq[db]);
         if (i == PREP && has_next) prep_finish(un, cur ^ 1);
-        if (i + 1 < NB) mwn = mask_word(u, i + 1);  // after this step's DMA: its wait (next step) covers only this
         if (LAST && cs_part) {
           // colsum(dQ)[d] over this unit = sum_w K_w^T cs_w: B operand = cs of the wave's keys (k)
           // in every column (wave-private LDS read-back), A = K_w^T from its image.
