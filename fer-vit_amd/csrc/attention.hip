@@ -1242,6 +1242,7 @@ __global__ __launch_bounds__(64 * NB) void attn_bwd_pers(
             cs += st[r];
           }
         }
+        BST(sb + 6 + 7 * i);
         char* Si = Sall + w * 2048;
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4)  // ds_off(lane & 31, 2 * g4 + hh) = dsb ^ (g4 << 4)
@@ -1255,6 +1256,7 @@ __global__ __launch_bounds__(64 * NB) void attn_bwd_pers(
             ot_[s2][db] = rd_trb(Oq + s2 * 2048, tb, db);
             qt_[s2][db] = rd_trb(Qq + s2 * 2048, tb, db);
           }
+        BST(sb + 7 + 7 * i);
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
           const bf16x8 pf = pack8(pd, s2), df = pack8(st, s2);

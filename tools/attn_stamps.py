@@ -80,7 +80,8 @@ def bwd():
     buf = (ctypes.c_ulonglong * (8 * 128))()
     assert lib().fer_debug_attn_bwd_stamps(buf) == 0
     st = [list(buf[w * 128:(w + 1) * 128]) for w in range(8)]
-    print("bwd p=0.1 (per step: s=start d=dS written b1=after barrier 1 q=dQ done b2=after barrier 2)")
+    print("bwd p=0.1 (per step: s=start v=P/dS VALU done t=dS written + dV/dK operand reads issued d=dV/dK MFMAs issued "
+          "b1=after barrier 1 q=dQ done b2=after barrier 2)")
     for u in (0, 1):
         o = u * 64
         base = min(st[w][o] for w in range(7) if st[w][o])
@@ -88,8 +89,8 @@ def bwd():
             row = st[w][o:o + 64]
             parts = []
             for i in range(7):
-                s0, d, b1, q, b2 = (row[1 + 7 * i + j] - base for j in range(5))
-                parts.append(f"[{s0}|{d}|{b1}|{q}|{b2}]")
+                s0, d, b1, q, b2, v, t = (row[1 + 7 * i + j] - base for j in range(7))
+                parts.append(f"[{s0}|{v}|{t}|{d}|{b1}|{q}|{b2}]")
             print(f"  unit{u} w{w} " + " ".join(parts) + f" last_loads={row[54] - base} epi: waited={row[50] - base} "
                   f"dq={row[51] - base} cs={row[52] - base} stg={row[53] - base} end={row[60] - base} out={row[61] - base}")
 
