@@ -512,13 +512,21 @@ __global__ __launch_bounds__(64 * (NB + 1)) void attn_fwd_pers(const bf16* __res
       {
         const float mul = dscale / l;
         const int so = __builtin_amdgcn_readfirstlane((int)((((long)b * N) * ldo + h * dh) * 2));
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
+        // 16-byte stores of chunk pairs through permlane32 swaps, as attn_fwd_occ
+        auto pack4 = [&](int i) {
           const f32x16& a = ot[i >> 2];
           const int g4 = i & 3;
           const bf16x4 v = {(bf16)(a[4 * g4] * mul), (bf16)(a[4 * g4 + 1] * mul), (bf16)(a[4 * g4 + 2] * mul),
                             (bf16)(a[4 * g4 + 3] * mul)};
-          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), ro, o_off(i, lane), so, 0);
+          return __builtin_bit_cast(u32x2, v);
+        };
+#pragma unroll
+        for (int i = 0; i < 8; i += 2) {
+          const u32x2 pk[2] = {pack4(i), pack4(i + 1)};
+          const auto x = __builtin_amdgcn_permlane32_swap(pk[0][0], pk[1][0], false, false);
+          const auto y = __builtin_amdgcn_permlane32_swap(pk[0][1], pk[1][1], false, false);
+          // o_off(i + hh, lane & 31): chunk i + hh of the row = d 8 (i + hh)
+          __builtin_amdgcn_raw_buffer_store_b128(u32x4{x[0], y[0], x[1], y[1]}, ro, o_off(i + hh, lane & 31), so, 0);
         }
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint((m + log2f(l)) * LN2), rl, lse_off,
                                               __builtin_amdgcn_readfirstlane(bh * N * 4), 0);
@@ -683,18 +691,32 @@ __global__ __launch_bounds__(64 * NB) __attribute__((amdgpu_waves_per_eu(4))) vo
   l = xhalf_sum(l);
   const float mul = dscale / l;
   const int so = __builtin_amdgcn_readfirstlane((int)((((long)b * N) * ldo + h * dh) * 2));
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
+  // 16-byte stores: lane half hh holds d = 8i + 4hh + {0..3} of its query row (i = 0..7); a permlane32
+  // swap per dword pairs the halves so that each lane stores whole 16-byte chunks i + hh of chunk pairs
+  // (i, i + 1) -- 4 dwordx4 stores per lane instead of 8 dwordx2 (the store tail is issue-bound)
+  auto pack4 = [&](int i) {
     const f32x16& a = ot[i >> 2];
     const int g4 = i & 3;
-    const int d = (i >> 2) * 32 + 8 * g4 + 4 * hh;
-    const uint32_t off = (((uint32_t)q * (uint32_t)ldo + (uint32_t)d) * 2u) | ((uint32_t)(q >= N || d >= dh) << 31);
     const bf16x4 v = {(bf16)(a[4 * g4] * mul), (bf16)(a[4 * g4 + 1] * mul), (bf16)(a[4 * g4 + 2] * mul),
                       (bf16)(a[4 * g4 + 3] * mul)};
-    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), ro, off, so, 0);
+    return __builtin_bit_cast(u32x2, v);
+  };
+  // lane terms re-derived here: computed in the prologue, the compiler kept them across the key loop (spilled)
+  const int le = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+  const int qe = w * 32 + (le & 31), he = le >> 5;
+#pragma unroll
+  for (int i = 0; i < 8; i += 2) {
+    const u32x2 pk[2] = {pack4(i), pack4(i + 1)};
+    const auto x = __builtin_amdgcn_permlane32_swap(pk[0][0], pk[1][0], false, false);
+    const auto y = __builtin_amdgcn_permlane32_swap(pk[0][1], pk[1][1], false, false);
+    // lanes 0-31: {own chunk i lo, partner's chunk i hi}; lanes 32-63: {partner's chunk i+1 lo, own hi}
+    const u32x4 c = {x[0], y[0], x[1], y[1]};
+    const int d = 8 * (i + he);
+    const uint32_t off = (((uint32_t)qe * (uint32_t)ldo + (uint32_t)d) * 2u) | ((uint32_t)(qe >= N || d >= dh) << 31);
+    __builtin_amdgcn_raw_buffer_store_b128(c, ro, off, so, 0);
   }
   __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint((m + log2f(l)) * LN2), rl,
-                                        (q < N && hh == 0) ? (uint32_t)(q * 4) : FER_OOB,
+                                        (qe < N && he == 0) ? (uint32_t)(qe * 4) : FER_OOB,
                                         __builtin_amdgcn_readfirstlane(bh * N * 4), 0);
 }
 
