@@ -1022,45 +1022,53 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_ring_kernel(GemmArgs g, 
     for (int j = 0; j < FM; ++j) af[j] = read_frag<MT, BM, AKC, RBK>(smem, wm * TM + j * MT, 0, lane);
   }
   static_assert(NST == 4, "vmcnt bookkeeping below assumes a 4-slot ring (PD = 3)");
-  for (int t = 0; t < nk; ++t) {
+  // One MFMA substep (t, kk) on fragments (ca, cb), the next substep's fragments read into (na, nb).
+  // The two fragment sets alternate by substep (SS = 2: within a K-step; SS = 1: the K loop unrolled by
+  // two): with one set copied forward at every substep's end, those copies were 48 v_mov per K-step
+  // (the loads into the next set are in flight while the MFMAs read the current one).
+  bf16x8 af1[FM], bf1[FN];
+  auto sub = [&](int t, int kk, const bf16x8 (&ca)[FM], const bf16x8 (&cb)[FN], bf16x8 (&na)[FM], bf16x8 (&nb)[FN]) {
     const char* cur = slot(t);
     const bool pf = t + PD < nk;
+    if (kk < SS - 1) {
 #pragma unroll
-    for (int kk = 0; kk < SS; ++kk) {
-      bf16x8 an[FM], bn[FN];
-      if (kk < SS - 1) {
+      for (int i = 0; i < FN; ++i) nb[i] = read_frag<MT, BN, BKC, RBK>(cur + A_BYTES, wn * TN + i * MT, kk + 1, lane);
 #pragma unroll
-        for (int i = 0; i < FN; ++i) bn[i] = read_frag<MT, BN, BKC, RBK>(cur + A_BYTES, wn * TN + i * MT, kk + 1, lane);
+      for (int j = 0; j < FM; ++j) na[j] = read_frag<MT, BM, AKC, RBK>(cur, wm * TM + j * MT, kk + 1, lane);
+      if (pf) issue_a(t + PD);
+    } else {
+      if (t + 1 < nk) {
+        // stage t+1 landed; stage t+2 and (SS>1) the A pieces of stage t+3 may be in flight
+        if (pf) wait_vm<PER + EARLY>();
+        else if (t + 2 < nk) wait_vm<PER>();
+        else wait_vm<0>();
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        const char* nx = slot(t + 1);
 #pragma unroll
-        for (int j = 0; j < FM; ++j) an[j] = read_frag<MT, BM, AKC, RBK>(cur, wm * TM + j * MT, kk + 1, lane);
-        if (pf) issue_a(t + PD);
-      } else {
-        if (t + 1 < nk) {
-          // stage t+1 landed; stage t+2 and (SS>1) the A pieces of stage t+3 may be in flight
-          if (pf) wait_vm<PER + EARLY>();
-          else if (t + 2 < nk) wait_vm<PER>();
-          else wait_vm<0>();
-          __builtin_amdgcn_s_barrier();
-          asm volatile("" ::: "memory");
-          const char* nx = slot(t + 1);
+        for (int i = 0; i < FN; ++i) nb[i] = read_frag<MT, BN, BKC, RBK>(nx + A_BYTES, wn * TN + i * MT, 0, lane);
 #pragma unroll
-          for (int i = 0; i < FN; ++i) bn[i] = read_frag<MT, BN, BKC, RBK>(nx + A_BYTES, wn * TN + i * MT, 0, lane);
-#pragma unroll
-          for (int j = 0; j < FM; ++j) an[j] = read_frag<MT, BM, AKC, RBK>(nx, wm * TM + j * MT, 0, lane);
-        }
-        if (pf) {
-          if (SS == 1) issue_a(t + PD);
-          issue_b(t + PD);
-        }
+        for (int j = 0; j < FM; ++j) na[j] = read_frag<MT, BM, AKC, RBK>(nx, wm * TM + j * MT, 0, lane);
       }
+      if (pf) {
+        if (SS == 1) issue_a(t + PD);
+        issue_b(t + PD);
+      }
+    }
 #pragma unroll
-      for (int j = 0; j < FM; ++j)
+    for (int j = 0; j < FM; ++j)
 #pragma unroll
-        for (int i = 0; i < FN; ++i) acc[i][j] = mfma<MT>(bfr[i], af[j], acc[i][j]);
-#pragma unroll
-      for (int i = 0; i < FN; ++i) bfr[i] = bn[i];
-#pragma unroll
-      for (int j = 0; j < FM; ++j) af[j] = an[j];
+      for (int i = 0; i < FN; ++i) acc[i][j] = mfma<MT>(cb[i], ca[j], acc[i][j]);
+  };
+  if constexpr (SS == 2) {
+    for (int t = 0; t < nk; ++t) {
+      sub(t, 0, af, bfr, af1, bf1);
+      sub(t, 1, af1, bf1, af, bfr);
+    }
+  } else {
+    for (int t = 0; t < nk; t += 2) {
+      sub(t, 0, af, bfr, af1, bf1);
+      if (t + 1 < nk) sub(t + 1, 0, af1, bf1, af, bfr);
     }
   }
   tile_epilogue<BM, BN, WM, WN, MT, EPC, NST * STAGE>(g, e, acc, smem, m0, n0, ks, wm, wn, lane);
