@@ -533,7 +533,7 @@ __device__ unsigned long long g_epst[2][16];
 // columns of one row: all global traffic of the epilogue is row-contiguous.
 template <int BM, int BN, int WM, int WN, int MT, int EPC, int SMEMB, int EK = EPI_GEN, typename AccT, int FN, int FM>
 FER_DEV void tile_epilogue(const GemmArgs& g, const EpiArgs& e, AccT (&acc)[FN][FM], char* smem, int m0, int n0,
-                           int ks, int wm, int wn, int lane) {
+                           int ks, int wm, int wn, int lane, uint64_t seed) {
   int tid_ = threadIdx.x;  // laundered: not hoisted out of a persistent tile loop
   asm volatile("" : "+v"(tid_));
 #ifdef FER_GEMM_STAMPS
@@ -594,7 +594,6 @@ FER_DEV void tile_epilogue(const GemmArgs& g, const EpiArgs& e, AccT (&acc)[FN][
     b1 = ldg_f32x4(e.bias + n + 4);
   }
   const float ps = e.post_scale ? *e.post_scale : 1.f;
-  const uint64_t seed = e.drop_thresh ? step_seed(e.seed) : 0;
   // fixed kinds (epi8_k): dropout scale folded into the bias / alpha (RES) or the GELU constants (GATE)
   constexpr bool KIND = EK != EPI_GEN;
   constexpr bool CS = !KIND || epi_base(EK) == EPI_MUL;  // only these kinds carry fused column sums
@@ -935,7 +934,8 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g, 
     }
   }
 
-  tile_epilogue<BM, BN, WM, WN, MT, (BM >= 256 ? 2 : 1), SMEM, EK>(g, e, acc, smem, m0, n0, ks, wm, wn, lane);
+  tile_epilogue<BM, BN, WM, WN, MT, (BM >= 256 ? 2 : 1), SMEM, EK>(g, e, acc, smem, m0, n0, ks, wm, wn, lane,
+                                                                     e.drop_thresh ? step_seed(e.seed) : 0);
 }
 
 // Ring variant: BK=32 stages in an NST-slot LDS ring, LDS-DMA issued NST-1 K-steps ahead and
@@ -1071,7 +1071,8 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_ring_kernel(GemmArgs g, 
       if (t + 1 < nk) sub(t + 1, 0, af1, bf1, af, bfr);
     }
   }
-  tile_epilogue<BM, BN, WM, WN, MT, EPC, NST * STAGE>(g, e, acc, smem, m0, n0, ks, wm, wn, lane);
+  tile_epilogue<BM, BN, WM, WN, MT, EPC, NST * STAGE>(g, e, acc, smem, m0, n0, ks, wm, wn, lane,
+                                                      e.drop_thresh ? step_seed(e.seed) : 0);
 }
 
 // ===================================================================== ping-pong kernel
@@ -1143,7 +1144,8 @@ __global__ __launch_bounds__(256, 2) void gemm_pp_kernel(GemmArgs g, EpiArgs e) 
       for (int i = 0; i < FN; ++i) acc[i][j] = mfma<MT>(bfr[i], af[j], acc[i][j]);
   }
   bar_lds();  // every wave's fragment reads are done: the ring becomes epilogue staging
-  tile_epilogue<BM, BN, WM, WN, MT, 2, NST * STAGE, EK>(g, e, acc, smem, m0, n0, ks, wm, wn, lane);
+  tile_epilogue<BM, BN, WM, WN, MT, 2, NST * STAGE, EK>(g, e, acc, smem, m0, n0, ks, wm, wn, lane,
+                                                         e.drop_thresh ? step_seed(e.seed) : 0);
 }
 
 template <bool AKC, bool BKC>
@@ -1267,7 +1269,7 @@ FER_DEV unsigned long long stamp_now() {
 // then the two wave-row halves through LDS.
 template <int EK>
 FER_DEV void tile_epilogue_wp(const GemmArgs& g, const EpiArgs& e, f32x4 (&acc)[4][8], char* smem, int m0, int n0,
-                              int wr, int wc, int lane) {
+                              int wr, int wc, int lane, uint64_t seed) {
   constexpr int S = epi_base(EK);
   constexpr bool X = S == EPI_RES || S == EPI_MUL;
   constexpr bool CS = S == EPI_MUL;
@@ -1281,7 +1283,6 @@ FER_DEV void tile_epilogue_wp(const GemmArgs& g, const EpiArgs& e, f32x4 (&acc)[
   const float dsc = e.drop_thresh ? e.drop_scale : 1.f;
   const float ab = (S == EPI_RES || EK == EPI_GATER) ? e.alpha * dsc : e.alpha;
   const f32x2 ghs = f32x2(0.5f * dsc), gps = f32x2(0.39894228040143268f * dsc);
-  const uint64_t seed = e.drop_thresh ? step_seed(e.seed) : 0;
   f32x4 b0 = f32x4{0.f, 0.f, 0.f, 0.f}, b1 = b0;
   if (e.bias && nok) {
     b0 = ldg_f32x4(e.bias + n);
@@ -1365,7 +1366,7 @@ FER_DEV void tile_epilogue_wp(const GemmArgs& g, const EpiArgs& e, f32x4 (&acc)[
 // prologue's operand DMA, and parks the id in that LDS word after the prologue's wait (which
 // retires the atomic together with the previous tile's epilogue stores and the first K-tile)
 template <bool AKC, bool BKC, int MT, int EK>
-FER_DEV void tile_8ph(const GemmArgs& g, const EpiArgs& e, int bid, char* smem, lds_vint* claim_slot) {
+FER_DEV void tile_8ph(const GemmArgs& g, const EpiArgs& e, int bid, char* smem, lds_vint* claim_slot, uint64_t seed) {
   typedef typename Acc<MT>::T AccT;
   constexpr int UNIT = 16384, BUF = 4 * UNIT;  // A0 A1 B0 B1
   constexpr int FM = 128 / MT, FN = 64 / MT;   // MFMA blocks per wave (rows, cols)
@@ -1497,9 +1498,9 @@ FER_DEV void tile_8ph(const GemmArgs& g, const EpiArgs& e, int bid, char* smem, 
   FER_STAMP(2);
   static_assert(64 * (256 + 4) * 4 <= 2 * BUF, "epilogue staging (2 chunks per half) must fit");
   if constexpr (EK != EPI_GEN && MT == 16)
-    tile_epilogue_wp<EK>(g, e, acc, smem, m0, n0, wr, wc, lane);
+    tile_epilogue_wp<EK>(g, e, acc, smem, m0, n0, wr, wc, lane, seed);
   else
-    tile_epilogue<256, 256, 2, 4, MT, 2, 2 * BUF, EK>(g, e, acc, smem, m0, n0, ks, wr, wc, lane);
+    tile_epilogue<256, 256, 2, 4, MT, 2, 2 * BUF, EK>(g, e, acc, smem, m0, n0, ks, wr, wc, lane, seed);
   FER_STAMP(3);
 #ifdef FER_GEMM_STAMPS
   if (st_on) {
@@ -1791,17 +1792,21 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph_kernel(GemmArgs g, EpiArgs e)
     };
     run(PpEpi{e.c, e.bias, (long)e.ldc, e.alpha});
   } else if constexpr (!DYN) {
+    // the dropout seed mixed with the step counter once per launch, not in every tile's epilogue
+    // (its global load and vmcnt(0) wait sat at the start of each epilogue)
+    const uint64_t seed = e.drop_thresh ? step_seed(e.seed) : 0;
 #pragma unroll 1
     for (int bid = blockIdx.x; bid < ntiles; bid += gridDim.x) {
-      tile_8ph<AKC, BKC, MT, EK>(g, e, bid, smem, nullptr);
+      tile_8ph<AKC, BKC, MT, EK>(g, e, bid, smem, nullptr, seed);
       bar_lds();  // every wave is done with the epilogue's LDS before the next tile's DMA
     }
   } else {
     lds_vint* slot = FER_LDS_INT(smem + 8 * 16384);
+    const uint64_t seed = e.drop_thresh ? step_seed(e.seed) : 0;
     int bid = wq_first(ntiles), par = 0;
 #pragma unroll 1
     while (bid >= 0) {
-      tile_8ph<AKC, BKC, MT, EK>(g, e, bid, smem, slot + par);
+      tile_8ph<AKC, BKC, MT, EK>(g, e, bid, smem, slot + par, seed);
       bar_lds();  // every wave is done with the epilogue's LDS before the next tile's DMA
       bid = __builtin_amdgcn_readfirstlane(slot[par]);
       par ^= 1;
