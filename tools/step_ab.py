@@ -15,6 +15,9 @@ over rounds. Variants:
   noadamcache    FusedAdamW uploads its segment table every step (the round-4 behaviour)
   lib:<k>=<v>    a library selector for the variant: attnfwd (fer_attention_set_fwd_kernel), gemmcfg
   env:<N>=<v>    environment variable N set to v for the variant (for switches the library reads per call)
+  hp             the step on a high-priority non-blocking stream (torch priority -1), weight gradients at the
+                 default priority (compare with nb:base)
+  hpwg           the opposite: the weight-gradient stream at high priority, the step on nb:base's stream
 <pred>: lt<N> (bit < N), ge<N> (bit >= N), m<K>lt<N> (bit % K < N), m<K>ge<N> (bit % K >= N).
 """
 import argparse
@@ -95,6 +98,9 @@ def main():
         return streams[pred]
 
     nb_compute = torch.cuda.Stream(device=dev)
+    hp_compute = torch.cuda.Stream(device=dev, priority=-1)
+    hp_side = torch.cuda.Stream(device=dev, priority=-1)
+    print("stream priority range", torch.cuda.Stream.priority_range(), flush=True)
     default_side = {}
 
     def setup(v):
@@ -124,6 +130,10 @@ def main():
             pass
         elif body == "wgoff":
             runtime.WGRAD.enabled = False
+        elif body == "hp":
+            cs = hp_compute
+        elif body == "hpwg":
+            runtime.WGRAD.streams[dev] = hp_side
         elif body == "adamwbw":  # optimizer step inside the backward (FusedAdamW.step_in_backward)
             opt.step_in_backward(True)
         elif body == "noadamcache":  # FusedAdamW re-uploads its segment table every step (round-4 behaviour)
