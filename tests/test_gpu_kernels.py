@@ -149,7 +149,8 @@ def test_gemm_every_tile_config(cfg):
     o = ops()
     lib().fer_gemm_set_config(cfg)
     try:
-        for M, N, K in [(300, 136, 200), (777, 520, 1096), (2056, 264, 520)]:
+        # (K = 24: a single K-step; the ring kernels' K loop runs two substeps per trip, odd counts included)
+        for M, N, K in [(300, 136, 200), (777, 520, 1096), (2056, 264, 520), (130, 72, 24)]:
             g = torch.Generator().manual_seed(M + cfg)
             x = torch.randn(M, K, generator=g)
             w = torch.randn(N, K, generator=g) / math.sqrt(K)
