@@ -1044,13 +1044,19 @@ __global__ __launch_bounds__(64 * NB) void attn_bwd_fused_bf16(const bf16* __res
 // 32-column block instead of a cross-lane reduction of the transposed dQ accumulators).
 // LDS (NB = 7): Q/dO images 2 x 56 KB, K images 28 KB, dS tiles 14 KB, lse/Dq 2 x 1.75 KB,
 // cs 0.9 KB = 158.4 KB.
+// From 6 key blocks up an extra (NB+1)-th wave prepares the next unit for every compute wave (LDS-DMA of
+// its dO / O rows and lse, Dq, the Q rows): it lands on the one SIMD that holds a single compute wave
+// (a workgroup's waves k and k+4 share a SIMD), so that work leaves the SIMDs of the critical waves.
+template <int NB> constexpr bool bwd_helper() { return NB >= 6; }
+template <int NB> constexpr int bwd_threads() { return 64 * (NB + (bwd_helper<NB>() ? 1 : 0)); }
+
 template <int NB>
 constexpr int pers_bwd_lds_bytes() {
   return 5 * NB * 4096 + NB * 2048 + 2 * 2 * NB * 32 * 4 + NB * 32 * 4;
 }
 
 template <int NB>
-__global__ __launch_bounds__(64 * NB) void attn_bwd_pers(
+__global__ __launch_bounds__(bwd_threads<NB>()) void attn_bwd_pers(
     const bf16* __restrict__ qkv, long ldq, const bf16* __restrict__ out, long ldo, const bf16* __restrict__ dout,
     long lddo, const float* __restrict__ lse, const uint32_t* __restrict__ mask, bf16* __restrict__ dqkv, long lddq,
     int BH, int N, int H, int dh, float scale, float sl2, float dscale, float* __restrict__ cs_part, WqArgs wq) {
@@ -1146,6 +1152,73 @@ __global__ __launch_bounds__(64 * NB) void attn_bwd_pers(
     u = blockIdx.x;
     un = u + (int)gridDim.x < BH ? u + (int)gridDim.x : -1;
   }
+  constexpr bool HELPER = bwd_helper<NB>();
+  if (HELPER && w == NB) {
+    // The helper wave: same barriers as the compute waves (prologue, two per step, one per unit), its
+    // own work in the first phase of steps 0-5 of every unit that has a next one (buffer cur ^ 1,
+    // free since the previous unit's last barrier): dO rows + lse | O rows | wait, Dq of rows 0-111 |
+    // Dq of rows 112-223 | Q rows of waves 0-3 over the O rows | Q rows of waves 4..NB-1.
+    bar_lds();
+    if (wq.q) un = __builtin_amdgcn_readfirstlane(hand[2]);
+#pragma unroll 1
+    for (int k = 0;; ++k) {
+      const int cur = k & 1, hb = cur ^ 1;
+      const bool has_next = un >= 0;
+#pragma unroll 1
+      for (int i = 0; i < NB; ++i) {
+        if (has_next && i < 6) {
+          const int b = un / H, h = un - b * H;
+          char* Qi = lds + hb * 2 * IMG;
+          float* L = lsd + hb * 2 * NB * 32;
+          if (i == 0) {
+#pragma unroll 1
+            for (int ww = 0; ww < NB; ++ww) {
+              img_dma_asm<NB>(Qi + IMG, rsrc4(dout), (long)b * N, lddo, h * dh, N, dh, ww, lane);
+              int ln = threadIdx.x & 63;
+              asm volatile("" : "+v"(ln));
+              const int r = ww * 32 + ln;
+              if (ln < 32) dma4_asm(L + ww * 32, rsrc4(lse + (long)un * N), r < N ? r * 4 : FER_OOB);
+            }
+          } else if (i == 1) {
+#pragma unroll 1
+            for (int ww = 0; ww < NB; ++ww) img_dma_asm<NB>(Qi, rsrc4(out), (long)b * N, ldo, h * dh, N, dh, ww, lane);
+          } else if (i == 2 || i == 3) {
+            if (i == 2) wait_vm<0>();
+#pragma unroll 1
+            for (int p = (i == 2 ? 0 : NB / 2); p < (i == 2 ? NB / 2 : NB); ++p) {
+              const int r = p * 32 + (lane >> 1), half = lane & 1;  // two lanes per row, 4 chunks each
+              float a = 0.f;
+#pragma unroll
+              for (int c = 0; c < 4; ++c) {
+                const bf16x8 o = rd_row(Qi, r, 4 * half + c), g = rd_row(Qi + IMG, r, 4 * half + c);
+#pragma unroll
+                for (int e = 0; e < 8; e += 2)
+                  a = __builtin_amdgcn_fdot2_f32_bf16(bf16x2{o[e], o[e + 1]}, bf16x2{g[e], g[e + 1]}, a, false);
+              }
+              a += __shfl_xor(a, 1, 64);
+              if (!half) {
+                L[NB * 32 + r] = -a;
+                L[r] = r < N ? -L[r] * inv_scale : -INFINITY;
+              }
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // O rows read: Q may land on them
+          } else {
+#pragma unroll 1
+            for (int ww = (i == 4 ? 0 : 4); ww < (i == 4 ? 4 : NB); ++ww)
+              img_dma_asm<NB>(Qi, rsrc4(qkv), (long)b * N, ldq, h * dh, N, dh, ww, lane);
+          }
+        }
+        bar_lds();  // dS tiles written
+        bar_lds();  // dS tiles and K images read
+      }
+      if (has_next) wait_vm<0>();  // the next unit's rows landed before the unit barrier
+      bar_lds();
+      u = un;
+      un = __builtin_amdgcn_readfirstlane(hand[cur]);
+      if (u < 0) break;
+    }
+    return;
+  }
   bf16x8 kf[4], vf[4];
   prep_issue(u, 0);
   load_frag(kf, u, D);
@@ -1205,7 +1278,7 @@ __global__ __launch_bounds__(64 * NB) void attn_bwd_pers(
         // pinned here: left to the compiler, the select sank below the LAST step's loads of the next
         // unit (and its exec-masked claim atomic) and waited vmcnt(0) for all of them (~4k cycles/unit)
         asm volatile("" : "+v"(mws)::"memory");
-        if (i == 0 && has_next) prep_issue(un, cur ^ 1);
+        if (!HELPER && i == 0 && has_next) prep_issue(un, cur ^ 1);
         // the next step's keep word, a whole step ahead of its use (issued in the dQ phase, its latency
         // was exposed at the next step's start: ~500 cycles per step); after this step's DMA, so the
         // next step's wait covers nothing issued later
@@ -1318,7 +1391,7 @@ __global__ __launch_bounds__(64 * NB) void attn_bwd_pers(
         for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
           for (int db = 0; db < 2; ++db) dq[db] = mfma32(kt[s2][db], sf[s2], dq[db]);
-        if (i == PREP && has_next) prep_finish(un, cur ^ 1);
+        if (!HELPER && i == PREP && has_next) prep_finish(un, cur ^ 1);
         if (LAST && cs_part) {
           // colsum(dQ)[d] over this unit = sum_w K_w^T cs_w: B operand = cs of the wave's keys (k)
           // in every column (wave-private LDS read-back), A = K_w^T from its image.
@@ -2064,7 +2137,7 @@ extern "C" int fer_attention_bwd(int dtype, const void* qkv, int64_t ld_qkv, con
     int occ = 1;
 #define FER_BOCC(NBV)                                                               \
   case NBV: {                                                                       \
-    static const int o = pers_occ(attn_bwd_pers<NBV>, 64 * NBV);                   \
+    static const int o = pers_occ(attn_bwd_pers<NBV>, bwd_threads<NBV>());                   \
     occ = o;                                                                        \
   } break;
     switch (nb) { FER_BOCC(1) FER_BOCC(2) FER_BOCC(3) FER_BOCC(4) FER_BOCC(5) FER_BOCC(6) FER_BOCC(7) }
@@ -2073,7 +2146,7 @@ extern "C" int fer_attention_bwd(int dtype, const void* qkv, int64_t ld_qkv, con
     const WqArgs wq = fixed_stride() ? WqArgs{} : wq_prepare_here(st, grid, B * H);
 #define FER_PERS(NBV)                                                                                          \
   case NBV:                                                                                                    \
-    hipLaunchKernelGGL(attn_bwd_pers<NBV>, dim3(grid), dim3(64 * NBV), 0, st, (const bf16*)qkv,                \
+    hipLaunchKernelGGL(attn_bwd_pers<NBV>, dim3(grid), dim3(bwd_threads<NBV>()), 0, st, (const bf16*)qkv,                \
                        (long)ld_qkv, (const bf16*)out, (long)ld_out, (const bf16*)dout, (long)ld_dout, lse, mask, \
                        (bf16*)dqkv, (long)ld_dqkv, B * H, N, H, dh, scale, sl2, drop_scale, colsum ? ws : nullptr, \
                        wq);                                                                                      \
