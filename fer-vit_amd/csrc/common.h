@@ -220,18 +220,25 @@ FER_DEV void gelu_and_grad8(f32x2 (&x)[4], f32x2 (&grad)[4]) {
 template <int P>
 FER_DEV void gelu_and_grad_ps(f32x2 (&x)[P], f32x2 (&grad)[P], f32x2 hs, f32x2 ps) {
   f32x2 e[P], z[P], t[P], y[P];
-  const f32x2 kh = kpk(-0.72134752044448170f);  // -log2(e) / 2
+  // z = |x| sqrt(log2(e) / 2): exp(-x^2/2) = exp2(-z^2), and |x| / sqrt(2) = z * 0.83255461 is folded
+  // into the A-S constant (one multiply per pair less than scaling x twice); the sign comes from x
+  const f32x2 kz = kpk(0.84932180028801907f);
 #pragma unroll
   for (int i = 0; i < P; ++i) {
-    const f32x2 h = x[i] * x[i] * kh;
-    e[i] = f32x2{__builtin_amdgcn_exp2f(h[0]), __builtin_amdgcn_exp2f(h[1])};
+    // |z| by two scalar multiplies with the abs modifier (packed f32 has none: v_and per element)
+    float z0 = __builtin_fabsf(x[i][0]) * kz[0], z1 = __builtin_fabsf(x[i][1]) * kz[1];
+    asm volatile("" : "+v"(z0), "+v"(z1));
+    z[i] = f32x2{z0, z1};
   }
 #pragma unroll
-  for (int i = 0; i < P; ++i) z[i] = x[i] * 0.70710678118654752f;
-  const f32x2 ka = kpk(0.3275911f);
+  for (int i = 0; i < P; ++i) {
+    const f32x2 h = -(z[i] * z[i]);
+    e[i] = f32x2{__builtin_amdgcn_exp2f(h[0]), __builtin_amdgcn_exp2f(h[1])};
+  }
+  const f32x2 ka = kpk(0.27273748087922250f);  // 0.3275911 / sqrt(2) / 0.84932180
 #pragma unroll
   for (int i = 0; i < P; ++i) {
-    const f32x2 d = __builtin_elementwise_fma(ka, __builtin_elementwise_abs(z[i]), f32x2(1.0f));
+    const f32x2 d = __builtin_elementwise_fma(ka, z[i], f32x2(1.0f));
     t[i] = f32x2{__builtin_amdgcn_rcpf(d[0]), __builtin_amdgcn_rcpf(d[1])};
   }
   const f32x2 k0 = kpk(1.061405429f), k1 = kpk(-1.453152027f);
@@ -249,7 +256,7 @@ FER_DEV void gelu_and_grad_ps(f32x2 (&x)[P], f32x2 (&grad)[P], f32x2 hs, f32x2 p
 #pragma unroll
   for (int i = 0; i < P; ++i) {
     const f32x2 r = 1.0f - y[i] * t[i] * e[i];
-    const f32x2 cdf = __builtin_elementwise_fma(hs, __builtin_elementwise_copysign(r, z[i]), hs);  // s * Phi(x)
+    const f32x2 cdf = __builtin_elementwise_fma(hs, __builtin_elementwise_copysign(r, x[i]), hs);  // s * Phi(x)
     grad[i] = __builtin_elementwise_fma(x[i] * ps, e[i], cdf);
     x[i] = x[i] * cdf;
   }
@@ -271,14 +278,16 @@ FER_DEV float act_grad(int act, float x) {
 // lowbias32 finaliser does the mixing: 2 integer multiplies per pair of elements.
 // Element indices are 32-bit: every C-ABI entry point with dropout checks idx < 2^32
 // (fer::check_drop_range); index arithmetic is done mod 2^32 by the callers.
-FER_DEV uint32_t fer_hash(uint64_t seed, uint32_t pair) {
-  uint32_t x = (pair ^ (uint32_t)seed) + (uint32_t)(seed >> 32);
+FER_DEV uint32_t fer_mix(uint32_t x) {  // the lowbias32 finaliser
   x ^= x >> 16;
   x *= 0x7FEB352Du;
   x ^= x >> 15;
   x *= 0x846CA68Bu;
   x ^= x >> 16;
   return x;
+}
+FER_DEV uint32_t fer_hash(uint64_t seed, uint32_t pair) {
+  return fer_mix((pair ^ (uint32_t)seed) + (uint32_t)(seed >> 32));
 }
 // Device-side step counter for graph-replayed training steps (fer_set_step_counter): a
 // captured launch keeps its host seed, so every dropout kernel mixes the current step into it.

@@ -157,6 +157,19 @@ FER_DEV void keep8(uint64_t seed, uint32_t idx, uint32_t thr, bool (&kp)[8]) {
   }
 }
 
+// keep8 for idx % 8 == 0 (the fixed kinds: 8-column pieces at n % 8 == 0, drop_ld % 8 == 0 checked by
+// epi_kind): the pair index p = idx / 2 is then a multiple of 4, so hash q's counter (p + q) ^ lo equals
+// (p ^ lo) ^ q -- one xor-add per hash instead of an add, a xor and an add. Same decisions as keep8.
+FER_DEV void keep8a(uint64_t seed, uint32_t idx, uint32_t thr, bool (&kp)[8]) {
+  const uint32_t thr_hi = thr << 16, a = (idx >> 1) ^ (uint32_t)seed, hi = (uint32_t)(seed >> 32);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint32_t h = fer_mix((a ^ (uint32_t)q) + hi);
+    kp[2 * q] = (h & 0xFFFFu) >= thr;
+    kp[2 * q + 1] = h >= thr_hi;
+  }
+}
+
 template <int S0>
 FER_DEV void epi8_t(const EpiArgs& e, long m, long n, f32x4& v0, f32x4& v1, f32x4 b0, f32x4 b1, bf16x8 x,
                     float ps, uint64_t seed) {
@@ -227,7 +240,7 @@ FER_DEV bf16x8 epi8_k(const E& e, uint32_t di, f32x4& v0, f32x4& v1, f32x4 b0, f
   if constexpr (S == EPI_GATER) {  // scale folded into ab / b (relu(x) * s = relu(x * s), s > 0)
     f32x4 g0, g1;
     bool kp[8];
-    if (e.drop_thresh) keep8(seed, di, e.drop_thresh, kp);
+    if (e.drop_thresh) keep8a(seed, di, e.drop_thresh, kp);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const bool k0 = e.drop_thresh ? kp[r] : true, k1 = e.drop_thresh ? kp[4 + r] : true;
@@ -246,7 +259,7 @@ FER_DEV bf16x8 epi8_k(const E& e, uint32_t di, f32x4& v0, f32x4& v1, f32x4 b0, f
     g0.xy = gs[0]; g0.zw = gs[1]; g1.xy = gs[2]; g1.zw = gs[3];
     if (e.drop_thresh) {
       bool kp[8];
-      keep8(seed, di, e.drop_thresh, kp);
+      keep8a(seed, di, e.drop_thresh, kp);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         v0[r] = kp[r] ? v0[r] : 0.f;
@@ -260,7 +273,7 @@ FER_DEV bf16x8 epi8_k(const E& e, uint32_t di, f32x4& v0, f32x4& v1, f32x4 b0, f
   if constexpr (S == EPI_RES) {
     if (e.drop_thresh) {
       bool kp[8];
-      keep8(seed, di, e.drop_thresh, kp);
+      keep8a(seed, di, e.drop_thresh, kp);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         v0[r] = kp[r] ? v0[r] : 0.f;
@@ -298,6 +311,7 @@ static inline bool epi_span_ok(const void* p, long ld, long M, long N) {
 }
 static inline int epi_kind(const EpiArgs& e, long M, long N) {
   if (e.c_f32 || e.accumulate || e.post_scale) return EPI_GEN;
+  if (e.drop_thresh && (e.drop_ld & 7)) return EPI_GEN;  // keep8a's index alignment
   if (!epi_span_ok(e.c, e.ldc, M, N) || !epi_span_ok(e.pre, e.ldp, M, N) || !epi_span_ok(e.res, e.ldr, M, N) ||
       !epi_span_ok(e.aux, e.ldx, M, N))
     return EPI_GEN;
