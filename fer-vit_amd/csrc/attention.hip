@@ -645,6 +645,10 @@ __global__ __launch_bounds__(64 * NB) __attribute__((amdgpu_waves_per_eu(4))) vo
     if (thr) {
       const uint32_t rw = TAIL ? drop_row(bh, N, w * 32 + (lv & 31)) : row;  // (re-derived: as lv)
       const uint32_t p0 = (rw >> 1) + kb * 16 + 2 * hh;
+      // the key's low word in a VGPR: with both key words in SGPRs the hash's counter step (pair ^ lo) + hi
+      // cannot be one v_xad_u32 (one scalar operand per VOP3), and costs an xor and an add per hash
+      uint32_t klo = (uint32_t)seed;
+      asm volatile("" : "+v"(klo));
       // two rounds of 8 ballots (16 SGPRs live instead of 32: the 16-ballot form spilled at 128 VGPRs)
       uint32_t word = 0u;
 #pragma unroll
@@ -657,7 +661,7 @@ __global__ __launch_bounds__(64 * NB) __attribute__((amdgpu_waves_per_eu(4))) vo
             bal[r] = bal[r + 1] = 0;
             continue;
           }
-          const uint32_t hv = fer_hash(seed, p0 + (uint32_t)(acc_row(rr, 0) >> 1));
+          const uint32_t hv = fer_mix(((p0 + (uint32_t)(acc_row(rr, 0) >> 1)) ^ klo) + (uint32_t)(seed >> 32));  // = fer_hash
           const bool k0 = (hv & 0xFFFFu) >= thr, k1 = (hv >> 16) >= thr;
           st[rr] = k0 ? st[rr] : 0.f;
           st[rr + 1] = k1 ? st[rr + 1] : 0.f;

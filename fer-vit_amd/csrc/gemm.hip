@@ -735,9 +735,9 @@ FER_DEV void tile_epilogue(const GemmArgs& g, const EpiArgs& e, AccT (&acc)[FN][
         epi8_kb<EK>(e, ok ? (uint32_t)m * ldcb + (uint32_t)n * 2 : FER_OOB, FER_OOB,
                    di0 + (uint32_t)(it * RPI) * (uint32_t)e.drop_ld, v0, v1, b0, b1, xr[it], seed, ab, ghs, gps, dsc,
                    rc, rp);
-        if constexpr (CS) {
-          cs0 += ok ? v0 : f32x4{0.f, 0.f, 0.f, 0.f};
-          cs1 += ok ? v1 : f32x4{0.f, 0.f, 0.f, 0.f};
+        if constexpr (CS) {  // no select: out-of-range rows multiply by zeros (x through FER_OOB), as in tile_epilogue_wp
+          cs0 += v0;
+          cs1 += v1;
         }
         v0 = n0;
         v1 = n1;
@@ -1346,9 +1346,11 @@ FER_DEV void tile_epilogue_wp(const GemmArgs& g, const EpiArgs& e, f32x4 (&acc)[
       epi8_kb<EK>(e, ok ? (uint32_t)row * ldcb + (uint32_t)n * 2 : FER_OOB,
                   ok ? (uint32_t)row * ldpb + (uint32_t)n * 2 : FER_OOB, di, v0, v1, b0, b1,
                   X ? xr[c & 1][p] : bf16x8{}, seed, ab, ghs, gps, dsc, rc, rp);
+      // no row / column select: an out-of-range row or column multiplies by its row operand x, loaded
+      // through FER_OOB as zeros, so it adds exactly 0 (its accumulators are 0 as well: zero-filled A rows)
       if constexpr (CS) {
-        cs0 += ok ? v0 : f32x4{0.f, 0.f, 0.f, 0.f};
-        cs1 += ok ? v1 : f32x4{0.f, 0.f, 0.f, 0.f};
+        cs0 += v0;
+        cs1 += v1;
       }
     }
   }
