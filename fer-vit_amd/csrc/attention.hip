@@ -661,8 +661,9 @@ __global__ __launch_bounds__(64 * NB) __attribute__((amdgpu_waves_per_eu(4))) vo
             bal[r] = bal[r + 1] = 0;
             continue;
           }
-          const uint32_t hv = fer_mix(((p0 + (uint32_t)(acc_row(rr, 0) >> 1)) ^ klo) + (uint32_t)(seed >> 32));  // = fer_hash
-          const bool k0 = (hv & 0xFFFFu) >= thr, k1 = (hv >> 16) >= thr;
+          uint32_t hlo;  // fer_hash's halves
+          const uint32_t hx = fer_mix_pre(((p0 + (uint32_t)(acc_row(rr, 0) >> 1)) ^ klo) + (uint32_t)(seed >> 32), hlo);
+          const bool k0 = hlo >= thr, k1 = (hx >> 16) >= thr;
           st[rr] = k0 ? st[rr] : 0.f;
           st[rr + 1] = k1 ? st[rr + 1] : 0.f;
           bal[r] = __builtin_amdgcn_ballot_w64(k0);

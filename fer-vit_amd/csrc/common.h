@@ -286,6 +286,17 @@ FER_DEV uint32_t fer_mix(uint32_t x) {  // the lowbias32 finaliser
   x ^= x >> 16;
   return x;
 }
+// fer_mix split for keep tests: returns x before the last step (h = x ^ (x >> 16) has x's high half, so
+// h >> 16 == x >> 16 and h >= t << 16 iff x >= t << 16) and sets lo = h & 0xFFFF by one SDWA xor (the
+// compiler's form is a shift and a bitop3)
+FER_DEV uint32_t fer_mix_pre(uint32_t x, uint32_t& lo) {
+  x ^= x >> 16;
+  x *= 0x7FEB352Du;
+  x ^= x >> 15;
+  x *= 0x846CA68Bu;
+  asm("v_xor_b32_sdwa %0, %1, %1 dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:WORD_0" : "=v"(lo) : "v"(x));
+  return x;
+}
 FER_DEV uint32_t fer_hash(uint64_t seed, uint32_t pair) {
   return fer_mix((pair ^ (uint32_t)seed) + (uint32_t)(seed >> 32));
 }

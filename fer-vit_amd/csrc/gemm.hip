@@ -164,9 +164,10 @@ FER_DEV void keep8a(uint64_t seed, uint32_t idx, uint32_t thr, bool (&kp)[8]) {
   const uint32_t thr_hi = thr << 16, a = (idx >> 1) ^ (uint32_t)seed, hi = (uint32_t)(seed >> 32);
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    const uint32_t h = fer_mix((a ^ (uint32_t)q) + hi);
-    kp[2 * q] = (h & 0xFFFFu) >= thr;
-    kp[2 * q + 1] = h >= thr_hi;
+    uint32_t lo;
+    const uint32_t x = fer_mix_pre((a ^ (uint32_t)q) + hi, lo);
+    kp[2 * q] = lo >= thr;
+    kp[2 * q + 1] = x >= thr_hi;
   }
 }
 
