@@ -197,6 +197,34 @@ def test_gemm_epilogue_bias_act_dropout_residual(act):
     assert rel_err(cs.cpu(), hh.grad.sum(0)) < 2e-2
 
 
+@pytest.mark.parametrize("drop_ld", [640, 644])
+@pytest.mark.parametrize("kind", ["gate", "res"])
+def test_gemm_epilogue_keep_bits_exact(kind, drop_ld):
+    """Every keep decision of the fused epilogues, element for element: the fixed kinds hash 8-element
+    pieces with keep8a when drop_ld % 8 == 0 (640); 644 takes the generic epilogue (csrc/gemm.hip
+    epi_kind). GATE: the output is exactly 0 where dropped and non-zero where kept (GELU of a
+    continuous pre-activation); RES: y - res isolates the dropped term (exactly 0 where dropped)."""
+    o = ops()
+    M, N, K, p, seed = 1030, 640, 384, 0.1, 0x1234_5678_9ABC
+    g = torch.Generator().manual_seed(11)
+    x, w = torch.randn(M, K, generator=g), torch.randn(N, K, generator=g) / math.sqrt(K)
+    b = torch.randn(N, generator=g)
+    keep = keep_mask(seed, (M, drop_ld), p)[:, :N]
+    h = bf(x).float().cpu() @ bf(w).float().cpu().t() + b
+    live = h.abs() < 4  # GELU's fp32 tail below about -5.3 rounds to exactly 0: not a keep decision
+    assert live.float().mean() > 0.99
+    if kind == "gate":
+        gate = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        y = o.linear_fwd(bf(x), bf(w), b.to(DEV), pre=gate, pre_gate=True, act="gelu", dropout=p, seed=seed,
+                         drop_ld=drop_ld).float().cpu()
+        got = y != 0
+    else:
+        res = torch.zeros(M, N, device=DEV, dtype=torch.bfloat16)  # y = drop(xW^T + b) exactly
+        y = o.linear_fwd(bf(x), bf(w), b.to(DEV), res=res, dropout=p, seed=seed, drop_ld=drop_ld).float().cpu()
+        got = y != 0
+    assert torch.equal(got[live], keep[live]), int((got != keep)[live].sum())
+
+
 @pytest.mark.parametrize("act", ["gelu", "relu"])
 @pytest.mark.parametrize("dtype", ["bf16", "fp32"])
 @pytest.mark.parametrize("p", [0.0, 0.1])
