@@ -1,5 +1,6 @@
 """Run one ViT-B GEMM a few times (PMC profiling target): GEMM_CASE=fc1 (K 768, plain) | fc2 (K 3072, plain) |
-fc1_fused (bias + GELU + dropout + pre). GEMM_CFG=<n>: force library config n (fer_gemm_set_config)."""
+fc1_fused (bias + GELU + dropout + pre) |
+fc1_gate (the model's fc1 forward: bias + GELU + dropout + gate, pre_gate). GEMM_CFG=<n>: force library config n (fer_gemm_set_config)."""
 import os
 import sys
 
@@ -30,6 +31,8 @@ for _ in range(6):
         ops.linear_fwd(x, w, out=out)
     elif case == "fc2":
         ops.linear_fwd(h, w2, out=y2)
+    elif case == "fc1_gate":
+        ops.linear_fwd(x, w, b, out=out, pre=pre, pre_gate=True, act="gelu", dropout=0.1, seed=7)
     else:
         ops.linear_fwd(x, w, b, out=out, pre=pre, act="gelu", dropout=0.1, seed=7)
 torch.cuda.synchronize()
